@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Benchmark: frame-pairs/sec of the DIS hot path at 1920x1080 preset=medium.
+
+One step = one call of the whole path (pyramid -> coarse-to-fine patch search
+-> densify -> upsample/crop) over a batch of synthetic u8 frame pairs already
+resident in HBM; outputs stay in HBM. Pairs shard across ranks (one process
+per GPU, launched by torch.distributed.run); there is no collective on the data
+path -- only the barrier and the max-over-ranks timing reduction.
+
+Prints ONE JSON line on rank 0 (contract in the task statement); extra fields:
+`roofline` for the dominant kernel (the patch-search kernel, all levels),
+`cpu_baseline` (the C oracle, one host core) and `max_epe_vs_oracle`.
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "optical-flow-using-dense-inverse-search_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import disflow  # noqa: E402
+
+METRIC = "frame-pairs/sec at 1920x1080 preset=medium, 1/2/4/8 GPUs; max EPE vs reference"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--preset", default="medium", choices=[p.name.lower() for p in disflow.Preset])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per search launch (from tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def make_pairs(seeds, W, H):
+    def one(s):
+        return disflow.synth_pair(int(s), W, H)
+
+    with cf.ThreadPoolExecutor(max_workers=min(16, len(seeds))) as ex:
+        res = list(ex.map(one, seeds))
+    return np.stack([a for a, _ in res]), np.stack([b for _, b in res])
+
+
+def cpu_baseline(params, W, H, budget_s):
+    """The C oracle (single host thread) on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_binding
+
+    n, t0 = 0, time.perf_counter()
+    while True:
+        I0, I1 = disflow.synth_pair(n, W, H)
+        t = time.perf_counter()
+        oracle_binding.calc_from_params(I0, I1, params)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s or n >= 64:
+            break
+        del t
+    el = time.perf_counter() - t0
+    return n, el
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    W, H, B = a.width, a.height, a.batch
+    params = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
+    wl = disflow.workload(params, W, H)
+
+    seeds = [rank * B + k for k in range(B)]
+    I0, I1 = make_pairs(seeds, W, H)
+    d0 = torch.from_numpy(I0).to(dev)
+    d1 = torch.from_numpy(I1).to(dev)
+    out = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
+    eng = disflow.DenseInverseSearch(params, W, H, max_batch=B, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), stream.cuda_stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.set_kernel_timing(True)
+    eng.kernel_time(disflow.KERNEL_SEARCH)  # reset accumulated records
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    el = time.perf_counter() - t0
+
+    n_s, ms_s = eng.kernel_time(disflow.KERNEL_SEARCH)
+    eng.set_kernel_timing(False)
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
+    el = float(el_t.item())
+
+    # parity spot check on rank 0: pair 0 of the last step vs the C oracle
+    max_epe = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_binding
+        exp = oracle_binding.calc_from_params(I0[0], I1[0], params)
+        got = out[0].cpu().numpy()
+        max_epe = float(np.sqrt(((got.astype(np.float64) - exp) ** 2).sum(-1)).max())
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        n, t = cpu_baseline(params, W, H, a.cpu_seconds)
+        cpu = {"value": n / t, "unit": "frame-pairs/s", "cores": 1, "kind": "port",
+               "sample": f"{n} synthetic {W}x{H} pairs (seeds 0..{n - 1}), preset={a.preset}, "
+                         f"C oracle (oracle/dis_oracle.c, gcc -O2 -ffp-contract=off), one host thread"}
+
+    avg_ms = ms_s / max(n_s, 1)
+    bytes_per_launch = B * wl["search_bytes_all"] / wl["search_launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if n_s else None
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            if tj.get("batch") == B and tj.get("width") == W and tj.get("preset") == a.preset:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        pairs = world * B * a.steps
+        line = {
+            "metric": METRIC,
+            "value": pairs / el,
+            "unit": "frame-pairs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": el / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded value-noise pairs warped by a smooth sinusoidal flow, dis_synth_pair)",
+            "config": {"workload": f"{W}x{H} preset={a.preset}, {B} pairs/GPU/step, inputs+outputs in HBM",
+                       "width": W, "height": H, "preset": a.preset, "global_batch": world * B,
+                       "knobs": {"C": params.coarsest_scale, "F": params.finest_scale, "ps": params.patch_size,
+                                 "it": params.iterations, "overlap": params.patch_overlap, "steps": wl["steps"]},
+                       "parallelism": f"pairs sharded over {world} rank(s), no data-path collective"},
+            "roofline": {"bound": "hbm", "kernel": "k_search (patch inverse search, all levels)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "avg_launch_ms": avg_ms, "launches": n_s,
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
+            "cpu_baseline": cpu,
+            "max_epe_vs_oracle": max_epe,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * dis_abi.h -- C-ABI of the MI355X-native DIS (Dense Inverse Search) optical
+ * flow engine. Plain C types only: pointers, sizes, ints, floats.
+ *
+ * The reference (nejcgalof/Optical-Flow-using-Dense-Inverse-Search) has no
+ * C-ABI or plugin interface; its hot path is reached through
+ *   (R1) construct_pyramide()                       src/main.cpp:12-50
+ *   (R2) OpticalFlow::OpticalFlowClass::ctor(...)   include/optical_flow.hpp:53-64,
+ *                                                   src/optical_flow.cpp:19-91
+ *   (R3) the pad / convert / upsample / crop glue   src/main.cpp:135-160, 191-198
+ * Each entry point below names the reference interface it replaces. The C++
+ * facade in include/dis/dis.hpp (DenseInverseSearch::calc and the
+ * OpticalFlow::OpticalFlowClass compatibility class) is built on these.
+ *
+ * Threading: a dis_ctx is bound to one HIP device; calls on one context must
+ * be serialised by the caller. Distinct contexts may run concurrently.
+ * Errors: every call returns a dis_status; dis_last_error() returns the
+ * calling thread's last error text. No C++ exception crosses this boundary.
+ */
+#ifndef DIS_ABI_H
+#define DIS_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DIS_ABI_VERSION 1
+
+typedef enum dis_status {
+    DIS_OK = 0,
+    DIS_ERR_INVALID_ARGUMENT = -1, /* bad parameter / pointer / size          */
+    DIS_ERR_UNSUPPORTED = -2,      /* valid request this build does not do     */
+    DIS_ERR_DEVICE = -3,           /* HIP runtime error or no usable device    */
+    DIS_ERR_OUT_OF_MEMORY = -4,    /* device or host allocation failed         */
+    DIS_ERR_INTERNAL = -5
+} dis_status;
+
+/* Build-defined presets (the reference has none). */
+typedef enum dis_preset {
+    DIS_PRESET_ULTRAFAST = 0, /* ps 8, overlap 0.5   (steps 4), it 12,  F 2, C auto */
+    DIS_PRESET_FAST = 1,      /* ps 8, overlap 0.5   (steps 4), it 16,  F 2, C auto */
+    DIS_PRESET_MEDIUM = 2,    /* ps 8, overlap 0.625 (steps 3), it 25,  F 1, C auto */
+    DIS_PRESET_SLOW = 3,      /* ps 8, overlap 0.75  (steps 2), it 128, F 0, C auto */
+    DIS_PRESET_REFERENCE = 4  /* CLI defaults src/main.cpp:66-71: ps 8, 0.7, it 1000, F 0, C 3 */
+} dis_preset;
+
+typedef enum dis_mem {
+    DIS_MEM_HOST = 0,  /* pointers are host memory: the call copies and synchronises */
+    DIS_MEM_DEVICE = 1 /* pointers are device memory on the context's device: the call
+                          is asynchronous on `stream` */
+} dis_mem;
+
+/* The reference's scalar knobs (src/optical_flow.cpp:19-31; CLI src/main.cpp:63-92). */
+typedef struct dis_params {
+    int coarsest_scale;      /* C: coarsest pyramid level, >= finest_scale              */
+    int finest_scale;        /* F: finest level searched; output upsampled by 2^F       */
+    int patch_size;          /* even, 2..16                                              */
+    int iterations;          /* >= 0; each patch does iterations+1 updates (Q3)          */
+    float patch_overlap;     /* [0,1); steps = max(1, floor(ps*(1-overlap))) in float    */
+    int patch_normalization; /* 0/1: mean-normalise the warped patch (src/patch.cpp:264) */
+    int var_refine_iters;    /* must be 0: the reference skips refinement (README.md:11) */
+} dis_params;
+
+typedef struct dis_ctx dis_ctx;
+
+/* Work/traffic figures of one frame pair (SURVEY.md 8d formula). */
+typedef struct dis_workload {
+    int padded_width, padded_height;
+    int steps;
+    long long patches;          /* sum of n_l over levels F..C                 */
+    long long updates;          /* sum of n_l*(iterations+1)                    */
+    double algorithmic_bytes;   /* SURVEY.md 8d "B" for one pair                */
+    double search_bytes_finest; /* 16*W_F*H_F + 16*n_F: the finest search launch */
+    double search_bytes_all;    /* sum over search launches (levels F..C) of
+                                   16*W_l*H_l + 16*n_l (+ 8*W_{l+1}*H_{l+1} coarse read) */
+    int search_launches;        /* C - F + 1 */
+} dis_workload;
+
+int dis_abi_version(void);
+const char* dis_last_error(void);
+
+/* Fill *out with the preset's knobs for a W x H input (C = auto rule). */
+dis_status dis_preset_params(dis_preset preset, int width, int height, dis_params* out);
+
+/* Validate knobs for a W x H input (what dis_create checks). */
+dis_status dis_validate_params(const dis_params* params, int width, int height);
+
+/* Work and algorithmic bytes per pair for these knobs. */
+dis_status dis_workload_info(const dis_params* params, int width, int height, dis_workload* out);
+
+/* Create a context for W x H u8 pairs on HIP device `device`, with device
+ * workspace for up to max_batch pairs per call (no allocation in calc). */
+dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int height,
+                      int max_batch, int device);
+dis_status dis_destroy(dis_ctx* ctx);
+
+/* One pair: u8 grayscale frames (row stride `stride` bytes, 0 = width) to a
+ * full-resolution W x H x 2 float flow, (u,v) interleaved, row-major.
+ * Replaces R3 + R1 + R2 for one pair (src/main.cpp:135-198). */
+dis_status dis_calc_u8(dis_ctx* ctx, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                       float* flow, dis_mem where, void* stream);
+
+/* n pairs in one call: pair k's frames at I0 + k*pair_stride (bytes), its
+ * flow at flow + k*W*H*2 floats. n <= max_batch. */
+dis_status dis_calc_batch_u8(dis_ctx* ctx, int n, const uint8_t* I0, const uint8_t* I1,
+                             size_t stride, size_t pair_stride, float* flow,
+                             dis_mem where, void* stream);
+
+/* Compatibility entry with the exact semantics of the reference constructor
+ * OpticalFlowClass(...) (include/optical_flow.hpp:53-64): host pyramids of
+ * (coarsest+1) PADDED planes (row stride W_l + 2*img_padding, pointer at the
+ * padded origin, as built by construct_pyramide, src/main.cpp:41-49), output
+ * `outflow` = (width>>F) x (height>>F) x 2 floats at the finest level.
+ * width/height must be multiples of 2^coarsest. The *_dx/_dy planes of the
+ * second frame are accepted and unused, as in the reference (Q15).
+ * Synchronous; runs on HIP device `device`. */
+dis_status dis_flow_from_pyramids(const float* const* img_first, const float* const* img_first_dx,
+                                  const float* const* img_first_dy, const float* const* img_second,
+                                  const float* const* img_second_dx, const float* const* img_second_dy,
+                                  int img_padding, float* outflow, int width, int height,
+                                  int coarsest_scale, int finest_scale, int iterations,
+                                  int patch_size, float patch_overlap, int patch_normalization,
+                                  int device);
+
+/* Stage dumps for parity tests: copy one intermediate of pair `pair` from the
+ * last calc on this context into host memory `dst` (count floats). Stages:
+ * level image frame 0 / frame 1, frame-0 Sobel dx / dy, per-patch u (n_l*2),
+ * dense flow (W_l*H_l*2). Requires dis_set_debug(ctx, 1) before the calc. */
+typedef enum dis_stage {
+    DIS_STAGE_IMG0 = 0,
+    DIS_STAGE_IMG1 = 1,
+    DIS_STAGE_DX0 = 2,
+    DIS_STAGE_DY0 = 3,
+    DIS_STAGE_PATCH_U = 4,
+    DIS_STAGE_DENSE = 5
+} dis_stage;
+dis_status dis_set_debug(dis_ctx* ctx, int enable);
+dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
+dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);
+
+/* Per-kernel timing with HIP events recorded on the context's launch stream
+ * around every launch of the named kernel class (bench / roofline use).
+ * kernel: 0 = pyramid, 1 = patch search (all levels), 2 = patch search
+ * (finest level only), 3 = densify + upsample. */
+dis_status dis_set_kernel_timing(dis_ctx* ctx, int enable);
+dis_status dis_kernel_time(dis_ctx* ctx, int kernel, int* launches, double* total_ms);
+
+/* Deterministic synthetic pair (SURVEY.md 8d generator): multi-octave value
+ * noise I0 and I1 = I0 warped by a smooth sinusoidal flow; optional
+ * ground-truth flow (W*H*2). Host memory, host compute; seed k -> pair k. */
+dis_status dis_synth_pair(uint64_t seed, int width, int height, uint8_t* I0, uint8_t* I1,
+                          float* gt_flow);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIS_ABI_H */

@@ -1,0 +1,53 @@
+// dis_kernels.h -- kernel argument blocks and host launchers.
+#pragma once
+
+#include "dis_common.h"
+
+namespace dis {
+
+// One patch-search launch: one level, a batch of pairs.
+struct SearchArgs {
+    const float* img0;         // frame-0 level planes (stack), for fused gradients
+    const float* img1;         // frame-1 level planes (stack)
+    const float* dx;           // frame-0 Sobel dx planes (stack)
+    const float* dy;           // frame-0 Sobel dy planes (stack)
+    const float2* dense_coarse;  // dense flow of level l+1 (nullptr at the coarsest level)
+    float2* u_out;             // patch displacements of level l
+    long long plane_stride;    // floats per pair
+    long long plane_off;       // this level's offset in the plane stack
+    long long dense_stride;    // float2 per pair (dense stack), dense_coarse pre-offset
+    long long u_stride;        // float2 per pair (patch stack), u_out pre-offset
+    int phys_pad;              // 0: virtual padding (clamp image / zero gradients);
+                               // >0: planes are physically padded by this many pixels
+                               //     (compat path), plane_off points at the padded origin
+    int W, H, steps, npw, nph, offw, offh, n;
+    float tmp_lb, tmp_ub_w, tmp_ub_h, outlier;
+    int iters, norm;
+};
+
+struct DensifyArgs {
+    const float2* u;       // patch u of the level (pre-offset)
+    float2* dense;         // dense flow of the level (pre-offset)
+    long long u_stride, dense_stride;
+    int W, H, ps, steps, npw, nph, offw, offh;
+};
+
+struct UpsampleArgs {
+    const float2* dense;   // finest-level dense flow (pre-offset)
+    float2* flow;          // W x H output, pair stride W*H
+    long long dense_stride;
+    int W, H, wF, hF, F, pad_left, pad_top, xmax;
+    float sc;
+    double inv_sc;
+};
+
+hipError_t launch_level0(const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,
+                         const Geometry& g, float* img0, float* img1, int batch, hipStream_t s);
+hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int batch, hipStream_t s);
+hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, float* dy, int batch,
+                        hipStream_t s);
+hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s);
+hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
+hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
+
+}  // namespace dis

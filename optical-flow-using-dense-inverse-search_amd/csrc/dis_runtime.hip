@@ -1,0 +1,672 @@
+// dis_runtime.hip -- the C-ABI (include/dis_abi.h): parameter validation,
+// geometry, device workspace and the per-batch launch sequence.
+//
+// The launch sequence is the reference's control flow restated for a batch of
+// pairs resident in HBM: src/main.cpp:135-198 (pad/convert, pyramid, upsample,
+// crop) around src/optical_flow.cpp:67-91 (coarse-to-fine scale loop).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "dis_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+dis_status fail(dis_status s, const std::string& msg)
+{
+    g_err = msg;
+    return s;
+}
+
+#define DIS_HIP(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(DIS_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+}  // namespace
+
+namespace dis {
+
+bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
+{
+    std::memset(g, 0, sizeof(*g));
+    g->W = W;
+    g->H = H;
+    g->C = p.coarsest_scale;
+    g->F = p.finest_scale;
+    g->ps = p.patch_size;
+    g->iters = p.iterations;
+    g->norm = p.patch_normalization ? 1 : 0;
+    // src/main.cpp:139-155
+    const int sf = 1 << g->C;
+    const int padw = (W % sf) ? sf - W % sf : 0;
+    const int padh = (H % sf) ? sf - H % sf : 0;
+    g->Wp = W + padw;
+    g->Hp = H + padh;
+    g->pad_left = padw / 2;
+    g->pad_top = padh / 2;
+    // src/optical_flow.cpp:490
+    const int st = (int)std::floor((float)p.patch_size * (1.0f - p.patch_overlap));
+    g->steps = st < 1 ? 1 : st;
+    long long poff = 0, uoff = 0, doff = 0;
+    for (int l = 0; l <= g->C; ++l) {
+        LevelGeom& L = g->lv[l];
+        const float sc = std::pow(2.0f, (float)-l);  // src/optical_flow.cpp:50-53
+        L.W = (int)((float)g->Wp * sc);
+        L.H = (int)((float)g->Hp * sc);
+        if (L.W < 1 || L.H < 1) return false;
+        L.steps = g->steps;
+        // src/patch_grid.cpp:20-23
+        L.npw = (int)std::ceil((float)L.W / (float)g->steps);
+        L.nph = (int)std::ceil((float)L.H / (float)g->steps);
+        L.offw = (L.W - (L.npw - 1) * g->steps) / 2;
+        L.offh = (L.H - (L.nph - 1) * g->steps) / 2;
+        L.n = L.npw * L.nph;
+        // src/optical_flow.cpp:55-57
+        L.tmp_lb = -(float)p.patch_size / 2;
+        L.tmp_ub_w = (float)(L.W + p.patch_size / 2 - 2);
+        L.tmp_ub_h = (float)(L.H + p.patch_size / 2 - 2);
+        L.plane_off = poff;
+        L.u_off = uoff;
+        L.dense_off = doff;
+        poff += (long long)L.W * L.H;
+        uoff += L.n;
+        doff += (long long)L.W * L.H;
+    }
+    g->plane_stride = (poff + 63) & ~63LL;
+    g->u_stride = (uoff + 31) & ~31LL;
+    g->dense_stride = (doff + 31) & ~31LL;
+    return true;
+}
+
+}  // namespace dis
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct dis_ctx {
+    dis_params p;
+    dis::Geometry g;
+    int device = 0;
+    int max_batch = 1;
+    int debug = 0;
+    int last_batch = 0;
+    hipStream_t own = nullptr;
+    // workspace (device)
+    float* img0 = nullptr;
+    float* img1 = nullptr;
+    float* dx = nullptr;
+    float* dy = nullptr;
+    float2* pu = nullptr;
+    float2* dense = nullptr;
+    uint8_t* in0 = nullptr;  // host-mode input staging
+    uint8_t* in1 = nullptr;
+    float2* out = nullptr;   // host-mode output staging
+    // kernel timing
+    int timing = 0;
+    struct Rec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<hipEvent_t> pool;
+    std::vector<Rec> recs;
+    size_t pool_next = 0;
+    int launches[4] = {0, 0, 0, 0};
+    double total_ms[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+dis_status check_params(const dis_params* p, int W, int H)
+{
+    if (!p) return fail(DIS_ERR_INVALID_ARGUMENT, "params is null");
+    if (W < 1 || H < 1) return fail(DIS_ERR_INVALID_ARGUMENT, "width and height must be >= 1");
+    if ((long long)W * H > (1LL << 28)) return fail(DIS_ERR_INVALID_ARGUMENT, "frame too large");
+    if (p->patch_size < 2 || p->patch_size > 16 || (p->patch_size & 1))
+        return fail(DIS_ERR_INVALID_ARGUMENT,
+                    "patch_size must be even and in [2,16] (odd sizes are broken in the reference, Q11)");
+    if (!(p->patch_overlap >= 0.0f && p->patch_overlap < 1.0f))
+        return fail(DIS_ERR_INVALID_ARGUMENT, "patch_overlap must be in [0,1)");
+    if (p->finest_scale < 0 || p->coarsest_scale < p->finest_scale)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "need 0 <= finest_scale <= coarsest_scale");
+    if (p->coarsest_scale >= dis::kMaxLevels - 1)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "coarsest_scale too large");
+    if (p->iterations < 0) return fail(DIS_ERR_INVALID_ARGUMENT, "iterations must be >= 0");
+    if (p->var_refine_iters != 0)
+        return fail(DIS_ERR_UNSUPPORTED, "variational refinement is not implemented (the reference skips it)");
+    const int sf = 1 << p->coarsest_scale;
+    const int Wp = W + ((W % sf) ? sf - W % sf : 0), Hp = H + ((H % sf) ? sf - H % sf : 0);
+    if ((Wp >> p->coarsest_scale) < 1 || (Hp >> p->coarsest_scale) < 1)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "frame smaller than 2^coarsest_scale");
+    return DIS_OK;
+}
+
+void free_ws(dis_ctx* c)
+{
+    hipFree(c->img0);
+    hipFree(c->img1);
+    hipFree(c->dx);
+    hipFree(c->dy);
+    hipFree(c->pu);
+    hipFree(c->dense);
+    hipFree(c->in0);
+    hipFree(c->in1);
+    hipFree(c->out);
+    c->img0 = c->img1 = c->dx = c->dy = nullptr;
+    c->pu = c->dense = c->out = nullptr;
+    c->in0 = c->in1 = nullptr;
+}
+
+// Kernel-timing bracket: records an event pair around one launch when enabled.
+struct TimeScope {
+    dis_ctx* c;
+    int kind;
+    hipStream_t s;
+    hipEvent_t b = nullptr;
+    TimeScope(dis_ctx* c_, int kind_, hipStream_t s_) : c(c_), kind(kind_), s(s_)
+    {
+        if (!c->timing || c->pool_next + 2 > c->pool.size()) return;
+        hipEvent_t a = c->pool[c->pool_next++];
+        b = c->pool[c->pool_next++];
+        hipEventRecord(a, s);
+        c->recs.push_back({kind, a, b});
+    }
+    ~TimeScope()
+    {
+        if (b) hipEventRecord(b, s);
+    }
+};
+
+// The whole path for n pairs already resident in device memory.
+dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                     size_t pair_stride, float2* flow, hipStream_t s)
+{
+    const dis::Geometry& g = c->g;
+    {
+        TimeScope t(c, 0, s);
+        DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, c->img0, c->img1, n, s));
+        for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+        for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, c->img0, c->dx, c->dy, n, s));
+    }
+    for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
+        const dis::LevelGeom& L = g.lv[l];
+        dis::SearchArgs a{};
+        a.img0 = c->img0;
+        a.img1 = c->img1;
+        a.dx = c->dx;
+        a.dy = c->dy;
+        a.dense_coarse = (l < g.C) ? c->dense + g.lv[l + 1].dense_off : nullptr;
+        a.u_out = c->pu + L.u_off;
+        a.plane_stride = g.plane_stride;
+        a.plane_off = L.plane_off;
+        a.dense_stride = g.dense_stride;
+        a.u_stride = g.u_stride;
+        a.phys_pad = 0;
+        a.W = L.W;
+        a.H = L.H;
+        a.steps = L.steps;
+        a.npw = L.npw;
+        a.nph = L.nph;
+        a.offw = L.offw;
+        a.offh = L.offh;
+        a.n = L.n;
+        a.tmp_lb = L.tmp_lb;
+        a.tmp_ub_w = L.tmp_ub_w;
+        a.tmp_ub_h = L.tmp_ub_h;
+        a.outlier = (float)g.ps / 2;
+        a.iters = g.iters;
+        a.norm = g.norm;
+        {
+            TimeScope t1(c, 1, s);
+            TimeScope t2(c, l == g.F ? 2 : -1, s);
+            DIS_HIP(dis::launch_search_generic(a, g.ps, n, s));
+        }
+        dis::DensifyArgs d{};
+        d.u = c->pu + L.u_off;
+        d.dense = c->dense + L.dense_off;
+        d.u_stride = g.u_stride;
+        d.dense_stride = g.dense_stride;
+        d.W = L.W;
+        d.H = L.H;
+        d.ps = g.ps;
+        d.steps = L.steps;
+        d.npw = L.npw;
+        d.nph = L.nph;
+        d.offw = L.offw;
+        d.offh = L.offh;
+        TimeScope t(c, 3, s);
+        DIS_HIP(dis::launch_densify(d, n, s));
+    }
+    {
+        const dis::LevelGeom& LF = g.lv[g.F];
+        dis::UpsampleArgs u{};
+        u.dense = c->dense + LF.dense_off;
+        u.flow = flow;
+        u.dense_stride = g.dense_stride;
+        u.W = g.W;
+        u.H = g.H;
+        u.wF = LF.W;
+        u.hF = LF.H;
+        u.F = g.F;
+        u.pad_left = g.pad_left;
+        u.pad_top = g.pad_top;
+        u.sc = std::pow(2.0f, (float)g.F);
+        u.inv_sc = 1.0 / (double)u.sc;
+        // xmax: first output column whose source index reaches wF-1 (HResizeLinear)
+        u.xmax = g.Wp;
+        for (int d = 0; d < g.Wp; ++d) {
+            float fx = (float)((d + 0.5) * u.inv_sc - 0.5);
+            int sx = (int)std::floor(fx);
+            if (sx < 0) sx = 0;
+            if (sx + 1 >= LF.W) {
+                u.xmax = d;
+                break;
+            }
+        }
+        TimeScope t(c, 3, s);
+        DIS_HIP(dis::launch_upsample(u, n, s));
+    }
+    c->last_batch = n;
+    return DIS_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// exported C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int dis_abi_version(void) { return DIS_ABI_VERSION; }
+
+const char* dis_last_error(void) { return g_err.c_str(); }
+
+dis_status dis_preset_params(dis_preset preset, int width, int height, dis_params* out)
+{
+    if (!out) return fail(DIS_ERR_INVALID_ARGUMENT, "out is null");
+    if (width < 1 || height < 1) return fail(DIS_ERR_INVALID_ARGUMENT, "width and height must be >= 1");
+    dis_params p{};
+    p.patch_size = 8;
+    p.patch_normalization = 1;
+    p.var_refine_iters = 0;
+    switch (preset) {
+        case DIS_PRESET_ULTRAFAST: p.patch_overlap = 0.5f; p.iterations = 12; p.finest_scale = 2; break;
+        case DIS_PRESET_FAST: p.patch_overlap = 0.5f; p.iterations = 16; p.finest_scale = 2; break;
+        case DIS_PRESET_MEDIUM: p.patch_overlap = 0.625f; p.iterations = 25; p.finest_scale = 1; break;
+        case DIS_PRESET_SLOW: p.patch_overlap = 0.75f; p.iterations = 128; p.finest_scale = 0; break;
+        case DIS_PRESET_REFERENCE:
+            // CLI defaults, src/main.cpp:66-71
+            p.patch_overlap = 0.7f; p.iterations = 1000; p.finest_scale = 0; p.coarsest_scale = 3;
+            *out = p;
+            return DIS_OK;
+        default: return fail(DIS_ERR_INVALID_ARGUMENT, "unknown preset");
+    }
+    // C = auto: integer division in min(W,H)/ps
+    const int mx = std::max(width, height), mn = std::min(width, height);
+    int c1 = (int)(std::log2((double)mx / (4.0 * p.patch_size)) + 0.5);
+    int c2 = (mn / p.patch_size) > 0 ? (int)std::log2((double)(mn / p.patch_size)) : 0;
+    int C = std::max(0, std::min(c1, c2));
+    p.coarsest_scale = C;
+    p.finest_scale = std::min(p.finest_scale, C);
+    *out = p;
+    return DIS_OK;
+}
+
+dis_status dis_validate_params(const dis_params* params, int width, int height)
+{
+    return check_params(params, width, height);
+}
+
+dis_status dis_workload_info(const dis_params* params, int width, int height, dis_workload* out)
+{
+    dis_status st = check_params(params, width, height);
+    if (st != DIS_OK) return st;
+    if (!out) return fail(DIS_ERR_INVALID_ARGUMENT, "out is null");
+    dis::Geometry g;
+    if (!dis::make_geometry(*params, width, height, &g)) return fail(DIS_ERR_INVALID_ARGUMENT, "bad geometry");
+    // SURVEY.md 8d fixed formula
+    double B = 2.0 * width * height;
+    long long patches = 0, updates = 0;
+    for (int l = 0; l <= g.C; ++l) B += 8.0 * g.lv[l].W * g.lv[l].H;
+    for (int l = g.F; l <= g.C; ++l) {
+        const double px = (double)g.lv[l].W * g.lv[l].H;
+        B += 8.0 * px;                               // frame-0 dx, dy
+        B += 16.0 * px + 16.0 * g.lv[l].n + 8.0 * px;  // search reads + u + dense write
+        patches += g.lv[l].n;
+        updates += (long long)g.lv[l].n * (g.iters + 1);
+    }
+    for (int l = g.F; l < g.C; ++l) B += 8.0 * g.lv[l + 1].W * g.lv[l + 1].H;
+    if (g.F > 0) B += 8.0 * g.lv[g.F].W * g.lv[g.F].H + 8.0 * width * height;
+    out->padded_width = g.Wp;
+    out->padded_height = g.Hp;
+    out->steps = g.steps;
+    out->patches = patches;
+    out->updates = updates;
+    out->algorithmic_bytes = B;
+    const dis::LevelGeom& LF = g.lv[g.F];
+    out->search_bytes_finest = 16.0 * LF.W * LF.H + 16.0 * LF.n;
+    double sb = 0.0;
+    for (int l = g.F; l <= g.C; ++l) {
+        sb += 16.0 * g.lv[l].W * g.lv[l].H + 16.0 * g.lv[l].n;
+        if (l < g.C) sb += 8.0 * g.lv[l + 1].W * g.lv[l + 1].H;
+    }
+    out->search_bytes_all = sb;
+    out->search_launches = g.C - g.F + 1;
+    return DIS_OK;
+}
+
+dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int height, int max_batch,
+                      int device)
+{
+    if (!out) return fail(DIS_ERR_INVALID_ARGUMENT, "out is null");
+    *out = nullptr;
+    dis_status st = check_params(params, width, height);
+    if (st != DIS_OK) return st;
+    if (max_batch < 1) return fail(DIS_ERR_INVALID_ARGUMENT, "max_batch must be >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return fail(DIS_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(DIS_ERR_INVALID_ARGUMENT, "device index out of range");
+    dis_ctx* c = new (std::nothrow) dis_ctx();
+    if (!c) return fail(DIS_ERR_OUT_OF_MEMORY, "host allocation failed");
+    c->p = *params;
+    c->device = device;
+    c->max_batch = max_batch;
+    if (!dis::make_geometry(*params, width, height, &c->g)) {
+        delete c;
+        return fail(DIS_ERR_INVALID_ARGUMENT, "bad geometry");
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        delete c;
+        return fail(DIS_ERR_DEVICE, "hipSetDevice failed");
+    }
+    const dis::Geometry& g = c->g;
+    const size_t B = (size_t)max_batch;
+    const size_t plane = sizeof(float) * (size_t)g.plane_stride * B;
+    bool ok = hipMalloc(&c->img0, plane) == hipSuccess && hipMalloc(&c->img1, plane) == hipSuccess &&
+              hipMalloc(&c->dx, plane) == hipSuccess && hipMalloc(&c->dy, plane) == hipSuccess &&
+              hipMalloc(&c->pu, sizeof(float2) * (size_t)g.u_stride * B) == hipSuccess &&
+              hipMalloc(&c->dense, sizeof(float2) * (size_t)g.dense_stride * B) == hipSuccess &&
+              hipMalloc(&c->in0, (size_t)width * height * B) == hipSuccess &&
+              hipMalloc(&c->in1, (size_t)width * height * B) == hipSuccess &&
+              hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
+        free_ws(c);
+        if (c->own) hipStreamDestroy(c->own);
+        delete c;
+        return fail(DIS_ERR_OUT_OF_MEMORY, "device workspace allocation failed");
+    }
+    *out = c;
+    return DIS_OK;
+}
+
+dis_status dis_destroy(dis_ctx* c)
+{
+    if (!c) return DIS_OK;
+    hipSetDevice(c->device);
+    if (c->own) hipStreamSynchronize(c->own);
+    free_ws(c);
+    for (hipEvent_t e : c->pool) hipEventDestroy(e);
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+    return DIS_OK;
+}
+
+dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                             size_t pair_stride, float* flow, dis_mem where, void* stream)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (!I0 || !I1 || !flow) return fail(DIS_ERR_INVALID_ARGUMENT, "null frame or flow pointer");
+    if (n < 1 || n > c->max_batch) return fail(DIS_ERR_INVALID_ARGUMENT, "n must be in [1, max_batch]");
+    const int W = c->g.W, H = c->g.H;
+    if (stride == 0) stride = (size_t)W;
+    if (stride < (size_t)W) return fail(DIS_ERR_INVALID_ARGUMENT, "stride < width");
+    if (pair_stride == 0) pair_stride = stride * H;
+    if (n > 1 && pair_stride < stride * H) return fail(DIS_ERR_INVALID_ARGUMENT, "pair_stride too small");
+    DIS_HIP(hipSetDevice(c->device));
+    if (where == DIS_MEM_DEVICE) {
+        return run_batch(c, n, I0, I1, stride, pair_stride, reinterpret_cast<float2*>(flow),
+                         reinterpret_cast<hipStream_t>(stream));
+    }
+    if (where != DIS_MEM_HOST) return fail(DIS_ERR_INVALID_ARGUMENT, "bad dis_mem");
+    hipStream_t s = c->own;
+    const size_t fsz = (size_t)W * H;
+    for (int k = 0; k < n; ++k) {
+        DIS_HIP(hipMemcpy2DAsync(c->in0 + k * fsz, W, I0 + k * pair_stride, stride, W, H,
+                                 hipMemcpyHostToDevice, s));
+        DIS_HIP(hipMemcpy2DAsync(c->in1 + k * fsz, W, I1 + k * pair_stride, stride, W, H,
+                                 hipMemcpyHostToDevice, s));
+    }
+    dis_status st = run_batch(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
+    if (st != DIS_OK) return st;
+    DIS_HIP(hipMemcpyAsync(flow, c->out, sizeof(float2) * fsz * n, hipMemcpyDeviceToHost, s));
+    DIS_HIP(hipStreamSynchronize(s));
+    return DIS_OK;
+}
+
+dis_status dis_calc_u8(dis_ctx* c, const uint8_t* I0, const uint8_t* I1, size_t stride, float* flow,
+                       dis_mem where, void* stream)
+{
+    return dis_calc_batch_u8(c, 1, I0, I1, stride, 0, flow, where, stream);
+}
+
+dis_status dis_set_debug(dis_ctx* c, int enable)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    c->debug = enable ? 1 : 0;  // this build always materialises every stage
+    return DIS_OK;
+}
+
+dis_status dis_stage_size(dis_ctx* c, int stage, int level, size_t* count)
+{
+    if (!c || !count) return fail(DIS_ERR_INVALID_ARGUMENT, "null argument");
+    const dis::Geometry& g = c->g;
+    if (level < 0 || level > g.C) return fail(DIS_ERR_INVALID_ARGUMENT, "level out of range");
+    const dis::LevelGeom& L = g.lv[level];
+    switch (stage) {
+        case DIS_STAGE_IMG0:
+        case DIS_STAGE_IMG1:
+        case DIS_STAGE_DX0:
+        case DIS_STAGE_DY0: *count = (size_t)L.W * L.H; return DIS_OK;
+        case DIS_STAGE_PATCH_U: *count = (size_t)L.n * 2; return DIS_OK;
+        case DIS_STAGE_DENSE: *count = (size_t)L.W * L.H * 2; return DIS_OK;
+        default: return fail(DIS_ERR_INVALID_ARGUMENT, "unknown stage");
+    }
+}
+
+dis_status dis_debug_dump(dis_ctx* c, int stage, int level, int pair, float* dst, size_t count)
+{
+    size_t need = 0;
+    dis_status st = dis_stage_size(c, stage, level, &need);
+    if (st != DIS_OK) return st;
+    if (!dst || count < need) return fail(DIS_ERR_INVALID_ARGUMENT, "dst null or too small");
+    if (pair < 0 || pair >= c->last_batch) return fail(DIS_ERR_INVALID_ARGUMENT, "pair not in last batch");
+    const dis::Geometry& g = c->g;
+    const dis::LevelGeom& L = g.lv[level];
+    if ((stage == DIS_STAGE_DX0 || stage == DIS_STAGE_DY0 || stage == DIS_STAGE_PATCH_U ||
+         stage == DIS_STAGE_DENSE) && level < g.F)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "stage not computed below finest_scale");
+    DIS_HIP(hipSetDevice(c->device));
+    DIS_HIP(hipDeviceSynchronize());
+    const void* src = nullptr;
+    switch (stage) {
+        case DIS_STAGE_IMG0: src = c->img0 + pair * g.plane_stride + L.plane_off; break;
+        case DIS_STAGE_IMG1: src = c->img1 + pair * g.plane_stride + L.plane_off; break;
+        case DIS_STAGE_DX0: src = c->dx + pair * g.plane_stride + L.plane_off; break;
+        case DIS_STAGE_DY0: src = c->dy + pair * g.plane_stride + L.plane_off; break;
+        case DIS_STAGE_PATCH_U: src = c->pu + pair * g.u_stride + L.u_off; break;
+        case DIS_STAGE_DENSE: src = c->dense + pair * g.dense_stride + L.dense_off; break;
+    }
+    DIS_HIP(hipMemcpy(dst, src, sizeof(float) * need, hipMemcpyDeviceToHost));
+    return DIS_OK;
+}
+
+dis_status dis_set_kernel_timing(dis_ctx* c, int enable)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    DIS_HIP(hipSetDevice(c->device));
+    if (enable && c->pool.empty()) {
+        c->pool.resize(8192);
+        for (auto& e : c->pool) DIS_HIP(hipEventCreate(&e));
+    }
+    c->timing = enable ? 1 : 0;
+    return DIS_OK;
+}
+
+dis_status dis_kernel_time(dis_ctx* c, int kernel, int* launches, double* total_ms)
+{
+    if (!c || kernel < 0 || kernel > 3) return fail(DIS_ERR_INVALID_ARGUMENT, "bad argument");
+    DIS_HIP(hipSetDevice(c->device));
+    for (auto& r : c->recs) {
+        DIS_HIP(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        DIS_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        if (r.kind >= 0 && r.kind < 4) {
+            c->launches[r.kind] += 1;
+            c->total_ms[r.kind] += ms;
+        }
+    }
+    c->recs.clear();
+    c->pool_next = 0;
+    if (launches) *launches = c->launches[kernel];
+    if (total_ms) *total_ms = c->total_ms[kernel];
+    return DIS_OK;
+}
+
+// Compat path: OpticalFlowClass(...) semantics over caller-padded host pyramids.
+dis_status dis_flow_from_pyramids(const float* const* img_first, const float* const* img_first_dx,
+                                  const float* const* img_first_dy, const float* const* img_second,
+                                  const float* const* img_second_dx, const float* const* img_second_dy,
+                                  int img_padding, float* outflow, int width, int height, int coarsest,
+                                  int finest, int iterations, int patch_size, float patch_overlap,
+                                  int patch_normalization, int device)
+{
+    (void)img_first;      // the template T is never used by the reference (Q2)
+    (void)img_second_dx;  // frame-2 gradients are never read (Q15)
+    (void)img_second_dy;
+    if (!img_first_dx || !img_first_dy || !img_second || !outflow)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "null pyramid or output pointer");
+    dis_params p{};
+    p.coarsest_scale = coarsest;
+    p.finest_scale = finest;
+    p.patch_size = patch_size;
+    p.iterations = iterations;
+    p.patch_overlap = patch_overlap;
+    p.patch_normalization = patch_normalization ? 1 : 0;
+    dis_status st = check_params(&p, width, height);
+    if (st != DIS_OK) return st;
+    if ((width % (1 << coarsest)) || (height % (1 << coarsest)))
+        return fail(DIS_ERR_INVALID_ARGUMENT, "width/height must be multiples of 2^coarsest");
+    if (img_padding < patch_size)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "img_padding must be >= patch_size");
+    for (int l = finest; l <= coarsest; ++l)
+        if (!img_first_dx[l] || !img_first_dy[l] || !img_second[l])
+            return fail(DIS_ERR_INVALID_ARGUMENT, "null plane in pyramid");
+    dis::Geometry g;
+    if (!dis::make_geometry(p, width, height, &g)) return fail(DIS_ERR_INVALID_ARGUMENT, "bad geometry");
+    // physically padded plane stacks
+    long long poff[dis::kMaxLevels], tot = 0;
+    for (int l = 0; l <= g.C; ++l) {
+        poff[l] = tot;
+        tot += (long long)(g.lv[l].W + 2 * img_padding) * (g.lv[l].H + 2 * img_padding);
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(DIS_ERR_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(DIS_ERR_INVALID_ARGUMENT, "device index out of range");
+    DIS_HIP(hipSetDevice(device));
+    float *dx = nullptr, *dy = nullptr, *i1 = nullptr;
+    float2 *pu = nullptr, *dense = nullptr;
+    auto cleanup = [&]() {
+        hipFree(dx);
+        hipFree(dy);
+        hipFree(i1);
+        hipFree(pu);
+        hipFree(dense);
+    };
+    if (hipMalloc(&dx, sizeof(float) * tot) != hipSuccess || hipMalloc(&dy, sizeof(float) * tot) != hipSuccess ||
+        hipMalloc(&i1, sizeof(float) * tot) != hipSuccess ||
+        hipMalloc(&pu, sizeof(float2) * g.u_stride) != hipSuccess ||
+        hipMalloc(&dense, sizeof(float2) * g.dense_stride) != hipSuccess) {
+        cleanup();
+        return fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
+    }
+    hipStream_t s = nullptr;
+    dis_status rc = DIS_OK;
+    auto H2D = [&](float* dst, const float* src, size_t cnt) {
+        return hipMemcpyAsync(dst, src, sizeof(float) * cnt, hipMemcpyHostToDevice, s);
+    };
+    for (int l = finest; l <= coarsest && rc == DIS_OK; ++l) {
+        const size_t cnt = (size_t)(g.lv[l].W + 2 * img_padding) * (g.lv[l].H + 2 * img_padding);
+        if (H2D(dx + poff[l], img_first_dx[l], cnt) != hipSuccess ||
+            H2D(dy + poff[l], img_first_dy[l], cnt) != hipSuccess ||
+            H2D(i1 + poff[l], img_second[l], cnt) != hipSuccess)
+            rc = fail(DIS_ERR_DEVICE, "pyramid upload failed");
+    }
+    for (int l = g.C; l >= g.F && rc == DIS_OK; --l) {
+        const dis::LevelGeom& L = g.lv[l];
+        dis::SearchArgs a{};
+        a.img1 = i1;
+        a.dx = dx;
+        a.dy = dy;
+        a.dense_coarse = (l < g.C) ? dense + g.lv[l + 1].dense_off : nullptr;
+        a.u_out = pu + L.u_off;
+        a.plane_stride = tot;
+        a.plane_off = poff[l];
+        a.dense_stride = g.dense_stride;
+        a.u_stride = g.u_stride;
+        a.phys_pad = img_padding;
+        a.W = L.W;
+        a.H = L.H;
+        a.steps = L.steps;
+        a.npw = L.npw;
+        a.nph = L.nph;
+        a.offw = L.offw;
+        a.offh = L.offh;
+        a.n = L.n;
+        a.tmp_lb = L.tmp_lb;
+        a.tmp_ub_w = L.tmp_ub_w;
+        a.tmp_ub_h = L.tmp_ub_h;
+        a.outlier = (float)g.ps / 2;
+        a.iters = g.iters;
+        a.norm = g.norm;
+        if (dis::launch_search_generic(a, g.ps, 1, s) != hipSuccess) {
+            rc = fail(DIS_ERR_DEVICE, "search launch failed");
+            break;
+        }
+        dis::DensifyArgs d{};
+        d.u = pu + L.u_off;
+        d.dense = dense + L.dense_off;
+        d.u_stride = g.u_stride;
+        d.dense_stride = g.dense_stride;
+        d.W = L.W;
+        d.H = L.H;
+        d.ps = g.ps;
+        d.steps = L.steps;
+        d.npw = L.npw;
+        d.nph = L.nph;
+        d.offw = L.offw;
+        d.offh = L.offh;
+        if (dis::launch_densify(d, 1, s) != hipSuccess) rc = fail(DIS_ERR_DEVICE, "densify launch failed");
+    }
+    if (rc == DIS_OK) {
+        const dis::LevelGeom& LF = g.lv[g.F];
+        if (hipMemcpyAsync(outflow, dense + LF.dense_off, sizeof(float2) * LF.W * LF.H, hipMemcpyDeviceToHost,
+                           s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = fail(DIS_ERR_DEVICE, "result download failed");
+    }
+    hipStreamSynchronize(s);
+    cleanup();
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle on
+the same inputs. The bar is BIT-EXACT float32 equality: the kernels evaluate
+the reference's float32 expressions in the reference's order (no FMA
+contraction, correctly rounded division and sqrt, Eigen's reduction order),
+so any difference is a bug, not rounding. (The oracle's own agreement with the
+reference is unpinned; see DESIGN.md.)"""
+import numpy as np
+import pytest
+
+import test_oracle as helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_bitexact(got, exp, what):
+    got = np.ascontiguousarray(got, np.float32)
+    exp = np.ascontiguousarray(exp, np.float32)
+    assert got.shape == exp.shape, (what, got.shape, exp.shape)
+    bad = got.view(np.uint32) != exp.view(np.uint32)
+    if bad.any():
+        idx = np.argwhere(bad)
+        d = np.abs(got.astype(np.float64) - exp.astype(np.float64))
+        raise AssertionError(f"{what}: {bad.sum()} of {bad.size} values differ; first at {idx[0].tolist()} "
+                             f"got {got[tuple(idx[0])]} exp {exp[tuple(idx[0])]}; max |diff| {np.nanmax(d)}")
+
+
+def _params(disflow, C, F, ps, it, overlap, norm=1):
+    return disflow.Params(coarsest_scale=C, finest_scale=F, patch_size=ps, iterations=it,
+                          patch_overlap=overlap, patch_normalization=norm)
+
+
+CASES = [
+    # (W, H, C, F, ps, it, overlap, norm)
+    (640, 480, 4, 2, 8, 12, 0.5, 1),      # config 1: ULTRAFAST 640x480
+    (160, 120, 3, 1, 8, 25, 0.625, 1),    # MEDIUM knobs, small
+    (203, 151, 3, 0, 8, 10, 0.7, 1),      # ragged size (padding), reference overlap
+    (96, 64, 2, 0, 4, 6, 0.5, 1),         # ps 4
+    (96, 64, 2, 1, 6, 5, 0.5, 0),         # ps 6, no normalization
+    (128, 96, 2, 0, 10, 4, 0.6, 1),       # ps 10
+    (64, 48, 1, 0, 16, 3, 0.75, 1),       # ps 16
+    (37, 29, 2, 2, 2, 3, 0.0, 1),         # ps 2, F == C
+    (64, 64, 3, 0, 8, 0, 0.5, 1),         # iterations 0 (one update)
+]
+
+
+@pytest.mark.parametrize("W,H,C,F,ps,it,overlap,norm", CASES)
+def test_end_to_end_bitexact(disflow_mod, oracle, W, H, C, F, ps, it, overlap, norm):
+    I0, I1 = disflow_mod.synth_pair(W * 7 + H, W, H)
+    p = _params(disflow_mod, C, F, ps, it, overlap, norm)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    got = eng.calc(I0, I1)
+    exp = oracle.calc_u8(I0, I1, C, F, ps, it, overlap, norm)
+    _assert_bitexact(got, exp, f"flow {W}x{H}")
+
+
+def test_large_shift_outliers_bitexact(disflow_mod, oracle):
+    # big translation: many patches hit the outlier reset / OOB start (Q4, Q5)
+    I0, I1 = helpers.shifted_pair(11, 120, 160, dx=9.5, dy=-7.25)
+    p = _params(disflow_mod, 2, 0, 8, 20, 0.5)
+    got = disflow_mod.DenseInverseSearch(p, 160, 120).calc(I0, I1)
+    _assert_bitexact(got, oracle.calc_u8(I0, I1, 2, 0, 8, 20, 0.5), "flow")
+
+
+def test_flat_image_singular_hessian(disflow_mod, oracle):
+    # constant frames: zero gradients, det == 0 regularisation (Q10)
+    I0 = np.full((48, 64), 77, np.uint8)
+    I1 = I0.copy()
+    I1[20:30, 20:40] = 200
+    p = _params(disflow_mod, 2, 0, 8, 5, 0.5)
+    got = disflow_mod.DenseInverseSearch(p, 64, 48).calc(I0, I1)
+    _assert_bitexact(got, oracle.calc_u8(I0, I1, 2, 0, 8, 5, 0.5), "flow")
+
+
+def test_stage_dumps_bitexact(disflow_mod, oracle):
+    W, H, C, F, ps, it, ov = 200, 136, 3, 1, 8, 8, 0.625
+    I0, I1 = disflow_mod.synth_pair(5, W, H)
+    eng = disflow_mod.DenseInverseSearch(_params(disflow_mod, C, F, ps, it, ov), W, H)
+    eng.set_debug(True)
+    eng.calc(I0, I1)
+    Wp, Hp, P0, PX, PY, P1, py0, py1 = oracle.build_pyramids(I0, I1, C, ps)
+    _, us, ds = oracle.flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, 1, capture=True)
+    S = disflow_mod
+    for l in range(C + 1):
+        _assert_bitexact(eng.debug_dump(S.STAGE_IMG0, l).reshape(py0[l][0].shape), py0[l][0], f"img0 l{l}")
+        _assert_bitexact(eng.debug_dump(S.STAGE_IMG1, l).reshape(py1[l][0].shape), py1[l][0], f"img1 l{l}")
+    for l in range(F, C + 1):
+        _assert_bitexact(eng.debug_dump(S.STAGE_DX0, l).reshape(py0[l][1].shape), py0[l][1], f"dx l{l}")
+        _assert_bitexact(eng.debug_dump(S.STAGE_DY0, l).reshape(py0[l][2].shape), py0[l][2], f"dy l{l}")
+        _assert_bitexact(eng.debug_dump(S.STAGE_PATCH_U, l).reshape(-1, 2), us[l], f"patch u l{l}")
+        _assert_bitexact(eng.debug_dump(S.STAGE_DENSE, l).reshape(ds[l].shape), ds[l], f"dense l{l}")
+
+
+def test_compat_constructor_path_bitexact(disflow_mod, oracle):
+    # OpticalFlowClass(...) semantics over caller-built padded pyramids
+    W, H, C, F, ps, it, ov = 160, 128, 3, 1, 8, 10, 0.7
+    I0, I1 = disflow_mod.synth_pair(21, W, H)
+    Wp, Hp, P0, PX, PY, P1, _, _ = oracle.build_pyramids(I0, I1, C, ps)
+    exp = oracle.flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, 1)
+    got = disflow_mod.optical_flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, True)
+    _assert_bitexact(got, exp, "compat flow")
+
+
+def test_batch_equals_single_and_deterministic(disflow_mod):
+    W, H = 176, 144
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    pairs = [disflow_mod.synth_pair(s, W, H) for s in range(4)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=4)
+    batch = eng.calc_batch(I0, I1)
+    again = eng.calc_batch(I0, I1)
+    assert np.array_equal(batch.view(np.uint32), again.view(np.uint32))
+    single = disflow_mod.DenseInverseSearch(p, W, H)
+    for k in range(4):
+        one = single.calc(I0[k], I1[k])
+        assert np.array_equal(one.view(np.uint32), batch[k].view(np.uint32)), k
+
+
+def test_device_resident_path(disflow_mod):
+    import torch
+    W, H = 320, 240
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    I0, I1 = disflow_mod.synth_pair(2, W, H)
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2)
+    host = eng.calc(I0, I1)
+    d0 = torch.from_numpy(np.stack([I0, I0])).cuda()
+    d1 = torch.from_numpy(np.stack([I1, I1])).cuda()
+    out = torch.empty((2, H, W, 2), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    eng.calc_device(2, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    o = out.cpu().numpy()
+    assert np.array_equal(o[0].view(np.uint32), host.view(np.uint32))
+    assert np.array_equal(o[1].view(np.uint32), host.view(np.uint32))
+
+
+def test_medium_1080p_full_size_bitexact(disflow_mod, oracle):
+    # BASELINE config 2 workload at full size against the oracle (a few seconds on CPU)
+    W, H = 1920, 1080
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    I0, I1, gt = disflow_mod.synth_pair(0, W, H, with_gt=True)
+    got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+    exp = oracle.calc_from_params(I0, I1, p)
+    _assert_bitexact(got, exp, "1080p medium flow")
+    epe = np.sqrt(((got - gt) ** 2).sum(-1))
+    assert np.median(epe) < 1.5  # the engine tracks the synthetic motion
+
+
+def test_invalid_calls_fail_loudly(disflow_mod):
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, 64, 64)
+    eng = disflow_mod.DenseInverseSearch(p, 64, 64, max_batch=1)
+    with pytest.raises(disflow_mod.DisError):
+        eng.calc_batch(np.zeros((2, 64, 64), np.uint8), np.zeros((2, 64, 64), np.uint8))
+    with pytest.raises(disflow_mod.DisError):
+        eng.debug_dump(disflow_mod.STAGE_DENSE, 0)  # nothing computed yet

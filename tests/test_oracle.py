@@ -1,0 +1,213 @@
+"""CPU tests of the oracle (the checker): it is compared with an independent
+numpy restatement (tests/pyref.py), with the reference's documented quirks
+ and with the committed golden fixtures (tests/golden/).
+
+Parity status: UNPINNED against the reference itself -- the reference has no
+tests, fixtures or golden vectors and cannot be built here (OpenCV 2.4 and
+Eigen 3 are absent); see DESIGN.md "Oracle".
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import pyref
+
+f32 = np.float32
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def smooth_noise(rng, H, W, blur=2):
+    a = rng.integers(0, 256, size=(H + 2 * blur, W + 2 * blur)).astype(np.float64)
+    k = np.ones(2 * blur + 1) / (2 * blur + 1)
+    a = np.apply_along_axis(lambda r: np.convolve(r, k, "valid"), 1, a)
+    a = np.apply_along_axis(lambda c: np.convolve(c, k, "valid"), 0, a)
+    a = (a - a.mean()) / (a.std() + 1e-9) * 45 + 128
+    return np.clip(np.round(a), 0, 255).astype(np.uint8)
+
+
+def shifted_pair(seed, H, W, dx=1.3, dy=-0.7):
+    rng = np.random.default_rng(seed)
+    big = smooth_noise(rng, H + 16, W + 16)
+    I0 = big[8:8 + H, 8:8 + W]
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    sx, sy = xx + 8 - dx, yy + 8 - dy
+    x0, y0 = np.floor(sx).astype(int), np.floor(sy).astype(int)
+    fx, fy = sx - x0, sy - y0
+    b = big.astype(np.float64)
+    v = (b[y0, x0] * (1 - fx) * (1 - fy) + b[y0, x0 + 1] * fx * (1 - fy)
+         + b[y0 + 1, x0] * (1 - fx) * fy + b[y0 + 1, x0 + 1] * fx * fy)
+    I1 = np.clip(np.round(v), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(I0), np.ascontiguousarray(I1)
+
+
+# --- reference quirks --------------------------------------
+
+def test_q8_ceil_epsilon_is_noop_from_256():
+    # ceil(x + 1e-5f) in float32 (src/patch.cpp:233-234)
+    assert np.ceil(f32(300) + f32(1e-5)) == 300
+    assert np.ceil(f32(200) + f32(1e-5)) == 201
+    first = next(i for i in range(1, 1000) if f32(i) + f32(1e-5) == f32(i))
+    assert first == 256
+
+
+def test_q12_steps_float_floor(oracle):
+    assert oracle.steps(12, 1.0 / 3.0) == 7   # float floor, not 8
+    assert oracle.steps(8, 0.7) == 2          # reference CLI default
+    assert oracle.steps(8, 0.625) == 3        # MEDIUM
+    assert oracle.steps(8, 0.5) == 4          # ULTRAFAST / FAST
+    assert oracle.steps(8, 0.95) == 1         # max(1, .)
+
+
+def test_grid_geometry_medium_1080p(oracle):
+    # level sizes and patch counts of SURVEY.md 8a row a7
+    counts = []
+    for l in range(1, 7):
+        npw, nph, _, _ = oracle.grid(1920 >> l, 1088 >> l, 3)
+        counts.append(npw * nph)
+    assert counts == [58240, 14560, 3680, 920, 240, 60]
+    assert sum(counts) == 77700
+
+
+def test_padding_split(oracle):
+    assert oracle.padded_size(1920, 1080, 6) == (1920, 1088, 0, 4)
+    assert oracle.padded_size(641, 483, 3) == (648, 488, 3, 2)
+
+
+# --- oracle vs independent numpy restatement --------------------------------
+
+@pytest.mark.parametrize("shape", [(24, 40), (33, 17), (8, 8)])
+def test_sobel_matches_numpy(oracle, shape):
+    rng = np.random.default_rng(1)
+    img = rng.random(shape, dtype=np.float32) * 255
+    dx, dy = oracle.sobel(img)
+    rx, ry = pyref.sobel(img)
+    assert np.array_equal(dx, rx) and np.array_equal(dy, ry)
+
+
+def test_pyramid_matches_numpy(oracle):
+    I0, _ = shifted_pair(3, 48, 64)
+    f0 = oracle.pad_convert(I0, 3)
+    got = oracle.pyramid(f0, 3)
+    ref = pyref.pyramid(f0, 3)
+    for (a, b, c), (x, y, z) in zip(got, ref):
+        assert np.array_equal(a, x) and np.array_equal(b, y) and np.array_equal(c, z)
+
+
+def test_level0_is_sobel_magnitude(oracle):
+    # Q1: the "image" at level 0 is sqrt(dx^2 + dy^2) of the input
+    I0, _ = shifted_pair(4, 32, 32)
+    f0 = oracle.pad_convert(I0, 2)
+    lv0 = oracle.pyramid(f0, 2)[0][0]
+    gx, gy = oracle.sobel(f0)
+    assert np.array_equal(lv0, np.sqrt(gx * gx + gy * gy))
+
+
+@pytest.mark.parametrize("ps,overlap,it,norm", [(8, 0.625, 4, 1), (4, 0.5, 3, 1), (6, 0.5, 2, 0),
+                                                (8, 0.7, 2, 1)])
+def test_patch_search_matches_numpy(oracle, ps, overlap, it, norm):
+    W, H, C, F = 64, 48, 2, 0
+    I0, I1 = shifted_pair(5, H, W)
+    Wp, Hp, P0, PX, PY, P1, py0, py1 = oracle.build_pyramids(I0, I1, C, ps)
+    out, us, ds = oracle.flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, overlap, norm,
+                                            capture=True)
+    st = oracle.steps(ps, overlap)
+    prev = None
+    for l in range(C, F - 1, -1):
+        w, h = Wp >> l, Hp >> l
+        if prev is None:
+            init = None
+        else:
+            def init(pid, rx, ry, prev=prev, w=w):
+                x, y = int(np.floor(rx / f32(2))), int(np.floor(ry / f32(2)))
+                v = prev[y, x]
+                return v[0] * f32(2), v[1] * f32(2)
+        u, geom = pyref.search_level(PX[l], PY[l], P1[l], ps, w, h, ps, st, it, norm, init)
+        assert np.array_equal(u, us[l]), f"patch u differs at level {l}"
+        d = pyref.densify(u, geom, w, h, ps, st)
+        assert np.array_equal(d, ds[l]), f"dense differs at level {l}"
+        prev = d
+    assert np.array_equal(out, ds[F])
+
+
+def test_upsample_matches_formula(oracle):
+    rng = np.random.default_rng(9)
+    for F in (1, 2):
+        Wp, Hp = 32, 24
+        fl = rng.standard_normal((Hp >> F, Wp >> F, 2)).astype(np.float32)
+        got = oracle.upsample_crop(fl, Wp, Hp, F, 0, 0, Wp, Hp)
+        # independent restatement of cv::resize INTER_LINEAR x2^F
+        s = fl * f32(2 ** F)
+        n_w, n_h = Wp >> F, Hp >> F
+
+        def coefs(nd, ns):
+            idx, fr, two = [], [], []
+            xmax = nd
+            for d in range(nd):
+                fx = f32((d + 0.5) * (1.0 / 2 ** F) - 0.5)
+                sx = int(np.floor(fx))
+                fx = f32(fx - f32(sx))
+                if sx < 0:
+                    fx, sx = f32(0), 0
+                if sx + 1 >= ns:
+                    xmax = min(xmax, d)
+                    if sx >= ns - 1:
+                        fx, sx = f32(0), ns - 1
+                idx.append(sx)
+                fr.append(fx)
+            return idx, fr, [d < xmax for d in range(nd)]
+
+        xi, xf, xt = coefs(Wp, n_w)
+        yi, yf, _ = coefs(Hp, n_h)
+        hrow = np.empty((n_h, Wp, 2), np.float32)
+        for x in range(Wp):
+            if xt[x]:
+                hrow[:, x] = s[:, xi[x]] * (f32(1) - xf[x]) + s[:, xi[x] + 1] * xf[x]
+            else:
+                hrow[:, x] = s[:, xi[x]]
+        exp = np.empty((Hp, Wp, 2), np.float32)
+        for y in range(Hp):
+            r1 = min(yi[y] + 1, n_h - 1)
+            exp[y] = hrow[yi[y]] * (f32(1) - yf[y]) + hrow[r1] * yf[y]
+        assert np.array_equal(got, exp)
+
+
+def test_q2_identical_frames_do_not_give_zero_flow(oracle):
+    # no template subtraction in the residual (src/patch.cpp:171-172)
+    I0, _ = shifted_pair(6, 64, 64)
+    flow = oracle.calc_u8(I0, I0, C=2, F=0, ps=8, it=8, overlap=0.5)
+    assert np.abs(flow).max() > 0.01
+
+
+def test_translation_is_recovered_roughly(oracle):
+    I0, I1 = shifted_pair(7, 96, 128, dx=1.5, dy=0.75)
+    flow = oracle.calc_u8(I0, I1, C=3, F=0, ps=8, it=16, overlap=0.5)
+    inner = flow[16:-16, 16:-16]
+    med = np.median(inner.reshape(-1, 2), axis=0)
+    # biased by Q2 but in the right direction and magnitude
+    assert 0.5 < med[0] < 2.5 and 0.2 < med[1] < 1.5
+
+
+def test_deterministic(oracle):
+    I0, I1 = shifted_pair(8, 48, 64)
+    a = oracle.calc_u8(I0, I1, C=2, F=1, ps=8, it=5, overlap=0.625)
+    b = oracle.calc_u8(I0, I1, C=2, F=1, ps=8, it=5, overlap=0.625)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# --- golden fixtures (regression lock of the oracle) ------------------------
+
+def _golden_files():
+    if not os.path.isdir(GOLDEN):
+        return []
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("name", _golden_files())
+def test_golden_fixture(oracle, name):
+    z = np.load(os.path.join(GOLDEN, name))  # allow_pickle=False (default)
+    C, F, ps, it, norm = (int(v) for v in z["knobs_i"])
+    overlap = float(z["knobs_f"][0])
+    flow = oracle.calc_u8(z["I0"], z["I1"], C=C, F=F, ps=ps, it=it, overlap=overlap, norm=norm)
+    assert np.array_equal(flow.view(np.uint32), z["flow"].view(np.uint32))
