@@ -74,7 +74,7 @@ def pad_convert(img_u8, C):
     Wp, Hp, _, _ = padded_size(W, H, C)
     out = np.empty((Hp, Wp), np.float32)
     a = np.ascontiguousarray(img_u8)
-    lib.dis_oracle_pad_convert(_p(a), W, H, W, C, _p(out))
+    lib.dis_oracle_pad_convert(_p(a), W, W, H, C, _p(out))
     return out
 
 

@@ -211,3 +211,12 @@ def test_golden_fixture(oracle, name):
     overlap = float(z["knobs_f"][0])
     flow = oracle.calc_u8(z["I0"], z["I1"], C=C, F=F, ps=ps, it=it, overlap=overlap, norm=norm)
     assert np.array_equal(flow.view(np.uint32), z["flow"].view(np.uint32))
+
+
+def test_pad_convert_matches_numpy(oracle):
+    # a1: replicate pad to a multiple of 2^C with floor/ceil split (src/main.cpp:139-160)
+    rng = np.random.default_rng(12)
+    img = rng.integers(0, 256, size=(151, 203), dtype=np.uint8)
+    got = oracle.pad_convert(img, 3)
+    exp = np.pad(img, ((0, 1), (2, 3)), mode="edge").astype(np.float32)  # 152 x 208
+    assert got.shape == (152, 208) and np.array_equal(got, exp)
