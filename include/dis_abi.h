@@ -138,6 +138,11 @@ typedef enum dis_stage {
     DIS_STAGE_DENSE = 5
 } dis_stage;
 dis_status dis_set_debug(dis_ctx* ctx, int enable);
+
+/* Kernel variant: 0 = auto (specialised kernels where available, e.g. the
+ * patch_size-8 search), 1 = generic kernels only. Both are bit-identical;
+ * the switch exists for parity tests and A/B timing. */
+dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
 dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);
 

@@ -1,0 +1,68 @@
+// dis_device.h -- device helpers shared by the DIS kernels (exact float32
+// semantics of the reference; compiled with -ffp-contract=off).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace dis {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// OpenCV BORDER_REFLECT_101 for an offset of at most one pixel outside [0, n).
+__device__ __forceinline__ int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
+}
+
+__device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
+// (src/patch.cpp:176): pivot on |a10| > |a00| (first index wins ties),
+// l = a_q0 / a_p0 (skipped when the pivot is 0), u11 = a_q1 - l * a_p1.
+struct LU2 {
+    float u00, u01, l10, u11;
+    int swap;
+};
+
+__device__ __forceinline__ LU2 lu2_factor(float h00, float h01, float h10, float h11)
+{
+    LU2 f;
+    f.swap = fabsf(h10) > fabsf(h00);
+    const float a00 = f.swap ? h10 : h00, a01 = f.swap ? h11 : h01;
+    const float a10 = f.swap ? h00 : h10, a11 = f.swap ? h01 : h11;
+    float l = a10;
+    if (a00 != 0.0f) l = a10 / a00;
+    f.u00 = a00;
+    f.u01 = a01;
+    f.l10 = l;
+    f.u11 = a11 - l * a01;
+    return f;
+}
+
+// PartialPivLU::solve: P b, unit-lower forward, upper backward substitution.
+__device__ __forceinline__ void lu2_solve(const LU2& f, float b0, float b1, float* x0, float* x1)
+{
+    float c0 = f.swap ? b1 : b0, c1 = f.swap ? b0 : b1;
+    c1 = c1 - f.l10 * c0;
+    c1 = c1 / f.u11;
+    c0 = c0 - c1 * f.u01;
+    c0 = c0 / f.u00;
+    *x0 = c0;
+    *x1 = c1;
+}
+
+// Hessian regularisation (src/patch.cpp:86-90): when the 2x2 determinant is
+// exactly zero, add the double literal 1e-10 to the diagonal (float += double).
+__device__ __forceinline__ LU2 hessian_lu2(float h00, float h01, float h11)
+{
+    const float h10 = h01;
+    if (h00 * h11 - h10 * h01 == 0.0f) {
+        h00 = (float)((double)h00 + 1e-10);
+        h11 = (float)((double)h11 + 1e-10);
+    }
+    return lu2_factor(h00, h01, h10, h11);
+}
+
+}  // namespace dis

@@ -25,6 +25,21 @@ struct SearchArgs {
     int iters, norm;
 };
 
+// Fast patch-size-8 search (dis_search8.hip): gradients fused from the level
+// image, init fused from the coarser level's patch displacements.
+struct Search8Args {
+    const float* img0;        // frame-0 level planes (stack)
+    const float* img1;        // frame-1 level planes (stack)
+    const float2* u_coarse;   // level l+1 patch u (pre-offset), nullptr at the coarsest level
+    float2* u_out;            // level l patch u (pre-offset)
+    long long plane_stride, plane_off, u_stride;
+    int W, H, steps, npw, nph, offw, offh;
+    int c_npw, c_nph, c_offw, c_offh;  // coarser level grid
+    float tmp_lb, tmp_ub_w, tmp_ub_h;
+    float thr_sq;             // largest float s with sqrtf(s) <= outlierthresh
+    int iters, norm;
+};
+
 struct DensifyArgs {
     const float2* u;       // patch u of the level (pre-offset)
     float2* dense;         // dense flow of the level (pre-offset)
@@ -47,6 +62,7 @@ hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int 
 hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, float* dy, int batch,
                         hipStream_t s);
 hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s);
+hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s);
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 

@@ -8,6 +8,7 @@
 // Batch: every kernel takes the pair index from blockIdx.z (or .y), so one
 // launch covers a whole batch of frame pairs (coarse levels have too few
 // patches per pair to fill 256 CUs otherwise).
+#include "dis_device.h"
 #include "dis_kernels.h"
 
 namespace dis {
@@ -15,16 +16,6 @@ namespace dis {
 // ---------------------------------------------------------------------------
 // Small exact-arithmetic helpers
 // ---------------------------------------------------------------------------
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// OpenCV BORDER_REFLECT_101 for an offset of at most one pixel.
-__device__ __forceinline__ int reflect101(int i, int n)
-{
-    if (n == 1) return 0;
-    i = i < 0 ? -i : i;
-    return i >= n ? 2 * n - 2 - i : i;
-}
 
 // Eigen 3.3 vectorized redux (4-wide SSE packets, two accumulators, aligned
 // storage) of N products x(0..N-1): src/patch.cpp:82-84, 171-172, 265.
@@ -65,39 +56,6 @@ __device__ __forceinline__ float eigen_sum(F&& x)
     }
 }
 
-// Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
-// (src/patch.cpp:176): pivot row p, l = a_q0/a_p0, u11 = a_q1 - l*a_p1.
-struct LU2 {
-    float u00, u01, l10, u11;
-    int swap;
-};
-
-__device__ __forceinline__ LU2 lu2_factor(float h00, float h01, float h10, float h11)
-{
-    LU2 f;
-    f.swap = fabsf(h10) > fabsf(h00);
-    float a00 = f.swap ? h10 : h00, a01 = f.swap ? h11 : h01;
-    float a10 = f.swap ? h00 : h10, a11 = f.swap ? h01 : h11;
-    float l = a10;
-    if (a00 != 0.0f) l = a10 / a00;
-    f.u00 = a00;
-    f.u01 = a01;
-    f.l10 = l;
-    f.u11 = a11 - l * a01;
-    return f;
-}
-
-__device__ __forceinline__ void lu2_solve(const LU2& f, float b0, float b1, float* x0, float* x1)
-{
-    float c0 = f.swap ? b1 : b0, c1 = f.swap ? b0 : b1;
-    c1 = c1 - f.l10 * c0;
-    c1 = c1 / f.u11;
-    c0 = c0 - c1 * f.u01;
-    c0 = c0 / f.u00;
-    *x0 = c0;
-    *x1 = c1;
-}
-
 // compute_hessian_matrix (src/patch.cpp:75-91) + factorisation.
 template <int NP>
 __device__ __forceinline__ LU2 hessian_lu(const float* gdx, const float* gdy)
@@ -105,12 +63,7 @@ __device__ __forceinline__ LU2 hessian_lu(const float* gdx, const float* gdy)
     float h00 = eigen_sum<NP>([&](int i) { return gdx[i] * gdx[i]; });
     float h01 = eigen_sum<NP>([&](int i) { return gdx[i] * gdy[i]; });
     float h11 = eigen_sum<NP>([&](int i) { return gdy[i] * gdy[i]; });
-    float h10 = h01;
-    if (h00 * h11 - h10 * h01 == 0.0f) {  // Eigen 2x2 determinant (:86)
-        h00 = (float)((double)h00 + 1e-10);  // float += double literal (:88-89)
-        h11 = (float)((double)h11 + 1e-10);
-    }
-    return lu2_factor(h00, h01, h10, h11);
+    return hessian_lu2(h00, h01, h11);
 }
 
 // ---------------------------------------------------------------------------
@@ -324,8 +277,6 @@ __global__ void __launch_bounds__(64) k_search_generic(SearchArgs a)
 // +0, weights 0.5 each (Q6, Q7: zero-initialised), then f /= w.
 // grid: (ceil(W/64), ceil(H/4), batch)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
-
 __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
 {
     const int x = blockIdx.x * 64 + threadIdx.x;

@@ -98,6 +98,7 @@ struct dis_ctx {
     int device = 0;
     int max_batch = 1;
     int debug = 0;
+    int variant = 0;  // 0 auto (fast kernels where available), 1 generic only
     int last_batch = 0;
     hipStream_t own = nullptr;
     // workspace (device)
@@ -185,16 +186,28 @@ struct TimeScope {
     }
 };
 
+// Largest float s with sqrtf(s) <= thr (sqrtf is correctly rounded and
+// monotone, so `sqrtf(s) > thr` <=> `s > thr_sq`; src/patch.cpp:185).
+float sqrt_threshold(float thr)
+{
+    float s = thr * thr;
+    while (std::sqrt(s) > thr) s = std::nextafter(s, 0.0f);
+    while (std::sqrt(std::nextafter(s, INFINITY)) <= thr) s = std::nextafter(s, INFINITY);
+    return s;
+}
+
 // The whole path for n pairs already resident in device memory.
 dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                      size_t pair_stride, float2* flow, hipStream_t s)
 {
     const dis::Geometry& g = c->g;
+    const bool fast = g.ps == 8 && c->variant == 0;
     {
         TimeScope t(c, 0, s);
         DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, c->img0, c->img1, n, s));
         for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
-        for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, c->img0, c->dx, c->dy, n, s));
+        if (!fast || c->debug)  // the fast search computes its template gradients itself
+            for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, c->img0, c->dx, c->dy, n, s));
     }
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         const dis::LevelGeom& L = g.lv[l];
@@ -224,11 +237,43 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         a.outlier = (float)g.ps / 2;
         a.iters = g.iters;
         a.norm = g.norm;
-        {
+        if (fast) {
+            dis::Search8Args b{};
+            b.img0 = c->img0;
+            b.img1 = c->img1;
+            b.u_coarse = (l < g.C) ? c->pu + g.lv[l + 1].u_off : nullptr;
+            b.u_out = c->pu + L.u_off;
+            b.plane_stride = g.plane_stride;
+            b.plane_off = L.plane_off;
+            b.u_stride = g.u_stride;
+            b.W = L.W;
+            b.H = L.H;
+            b.steps = L.steps;
+            b.npw = L.npw;
+            b.nph = L.nph;
+            b.offw = L.offw;
+            b.offh = L.offh;
+            if (l < g.C) {
+                b.c_npw = g.lv[l + 1].npw;
+                b.c_nph = g.lv[l + 1].nph;
+                b.c_offw = g.lv[l + 1].offw;
+                b.c_offh = g.lv[l + 1].offh;
+            }
+            b.tmp_lb = L.tmp_lb;
+            b.tmp_ub_w = L.tmp_ub_w;
+            b.tmp_ub_h = L.tmp_ub_h;
+            b.thr_sq = sqrt_threshold((float)g.ps / 2);
+            b.iters = g.iters;
+            b.norm = g.norm;
+            TimeScope t1(c, 1, s);
+            TimeScope t2(c, l == g.F ? 2 : -1, s);
+            DIS_HIP(dis::launch_search8(b, n, s));
+        } else {
             TimeScope t1(c, 1, s);
             TimeScope t2(c, l == g.F ? 2 : -1, s);
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s));
         }
+        if (fast && !c->debug && l != g.F) continue;  // dense flow only needed at the finest level
         dis::DensifyArgs d{};
         d.u = c->pu + L.u_off;
         d.dense = c->dense + L.dense_off;
@@ -463,6 +508,14 @@ dis_status dis_set_debug(dis_ctx* c, int enable)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
     c->debug = enable ? 1 : 0;  // this build always materialises every stage
+    return DIS_OK;
+}
+
+dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (variant < 0 || variant > 1) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0 or 1");
+    c->variant = variant;
     return DIS_OK;
 }
 

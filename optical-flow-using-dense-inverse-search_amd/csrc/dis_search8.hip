@@ -1,0 +1,335 @@
+// dis_search8.hip -- K3 fast path: patch inverse search for patch_size 8.
+//
+// Implements, for one pyramid level and a batch of pairs, the reference's
+//   PatchGrid::patch_init_from_prev_flow   src/patch_grid.cpp:108-119 (fused:
+//       densified coarser flow evaluated only at the sampled pixel),
+//   Patch::init_patch (template gradients)  src/patch.cpp:31-91 (fused: Sobel
+//       of the level image computed on the fly, src/main.cpp:34-35),
+//   Patch::inverse_search                   src/patch.cpp:119-203,
+//   Patch::get_patch_second_image           src/patch.cpp:207-267.
+//
+// Mapping (CDNA4, wave64): 4 lanes per patch, 16 patches per wave; lane q of a
+// patch owns pixel columns q and q+4 (8 rows each). Eigen's SSE reduction of a
+// 64-vector (two 4-wide packet accumulators) is then exact:
+//   A_c  = sequential sum down column c          (in-lane, 7 adds)
+//   C_q  = A_q + A_{q+4}                          (in-lane)
+//   sum  = (C_0 + C_2) + (C_1 + C_3)              (two DPP quad_perm adds)
+// A workgroup (4 waves) owns an 8x8 block of the patch grid and stages the
+// target image region every one of its patches can sample (start +-4 px,
+// SURVEY.md 7.3 "I1 search window") into one shared LDS tile. When the block's
+// start positions are too spread for the tile, the same arithmetic reads the
+// level plane through L1/L2 instead (identical results, slower).
+#include "dis_device.h"
+#include "dis_kernels.h"
+
+namespace dis {
+
+namespace {
+
+constexpr int kBG = 8;             // patch-grid block per workgroup: kBG x kBG patches
+constexpr int kTileMax = 64;       // max staged tile edge (pixels)
+constexpr int kTS = kTileMax + 1;  // tile row stride (floats): odd -> fewer bank conflicts
+
+// quad_perm DPP controls
+constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;  // [2,3,0,1]
+
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Eigen-order sum of the patch's 64 values held as x[0..7] (column q, rows
+// 0..7) and x[8..15] (column q+4) in each of the patch's 4 lanes.
+__device__ __forceinline__ float patch_sum(const float (&x)[16])
+{
+    float a = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) a = a + x[j];
+    float b = x[8];
+#pragma unroll
+    for (int j = 9; j < 16; ++j) b = b + x[j];
+    const float c = a + b;                        // C_q = A_q + A_{q+4}
+    const float t = c + quad_perm<kQuadXor2>(c);  // C_q + C_{q^2}
+    return t + quad_perm<kQuadXor1>(t);           // (C0+C2) + (C1+C3)
+}
+
+template <typename Fn>
+__device__ __forceinline__ float patch_dot(const float (&g)[16], Fn&& r)
+{
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = g[j] * r(j);
+    return patch_sum(x);
+}
+
+// Wave-wide min/max of an int (all 64 lanes participate).
+__device__ __forceinline__ int wave_min(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Bilinear warp + mean normalisation (src/patch.cpp:207-267) for one patch
+// position; `tap(row, col)` returns the target image at (Y-5+row, X-5+q+col)
+// relative rows 0..8 and relative cols {0,1} (set 0) / {4,5} (set 1).
+struct Warp {
+    float w0, w1, w2, w3;
+    int X, Y;
+};
+
+__device__ __forceinline__ Warp warp_coefs(float x, float y)
+{
+    Warp w;
+    const float l = floorf(x), k = floorf(y);
+    const float a = x - l, b = y - k;
+    w.w0 = (1 - a) * (1 - b);
+    w.w1 = a * (1 - b);
+    w.w2 = b * (1 - a);
+    w.w3 = a * b;
+    w.X = (int)ceilf(x + .00001f);  // Q8: the epsilon is a no-op from 256 on
+    w.Y = (int)ceilf(y + .00001f);
+    return w;
+}
+
+template <typename Tap>
+__device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[16])
+{
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float vb[9], va[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            vb[k] = tap(k, 4 * s);      // column X-5+c  (B / D taps)
+            va[k] = tap(k, 4 * s + 1);  // column X-4+c  (A / C taps)
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            // row Y-4+j: A = va[j+1], B = vb[j+1]; row Y-5+j: C = va[j], D = vb[j]
+            float t = w.w3 * va[j + 1];
+            t = t + w.w2 * vb[j + 1];
+            t = t + w.w1 * va[j];
+            t = t + w.w0 * vb[j];
+            r[8 * s + j] = t;
+        }
+    }
+    if (norm) {
+        const float mean = patch_sum(r) / 64.0f;  // sum / num_points_patch (:265)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r[j] = r[j] - mean;
+    }
+}
+
+// The per-patch iteration (src/patch.cpp:156-203) with a given tap source.
+template <typename TapAt>
+__device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[16],
+                                        const float (&gy)[16], float rx, float ry, float ix, float iy,
+                                        float* pu0, float* pu1, TapAt&& tap_at)
+{
+    float u0 = ix, u1 = iy;
+    const float sx = rx + u0, sy = ry + u1;
+    float r[16];
+    Warp w = warp_coefs(sx, sy);
+    warp_patch(w, a.norm, tap_at(w), r);
+    for (int counter = 1;; ++counter) {
+        const float b0 = patch_dot(gx, [&](int j) { return r[j]; });
+        const float b1 = patch_dot(gy, [&](int j) { return r[j]; });
+        float d0, d1;
+        lu2_solve(lu, b0, b1, &d0, &d1);
+        u0 = u0 - d0;
+        u1 = u1 - d1;
+        const float px = rx + u0, py = ry + u1;
+        const float ex = sx - px, ey = sy - py;
+        const float s2 = ex * ex + ey * ey;
+        // sqrtf(s2) > outlierthresh  <=>  s2 > thr_sq (sqrt is correctly rounded
+        // and monotone; thr_sq precomputed on the host); NaN -> reset (see oracle)
+        if (s2 > a.thr_sq || s2 != s2 || px < a.tmp_lb || py < a.tmp_lb || px > a.tmp_ub_w ||
+            py > a.tmp_ub_h) {
+            u0 = ix;
+            u1 = iy;
+            break;
+        }
+        if (counter > a.iters) break;
+        w = warp_coefs(px, py);
+        warp_patch(w, a.norm, tap_at(w), r);
+    }
+    *pu0 = u0;
+    *pu1 = u1;
+}
+
+}  // namespace
+
+// grid: (ceil(npw/8), ceil(nph/8), batch); block 256
+__global__ void __launch_bounds__(256) k_search8(Search8Args a)
+{
+    __shared__ float tile[kTileMax * kTS];
+    __shared__ int bnd[4];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int q = lane & 3, pw = lane >> 2;  // lane in patch, patch in wave
+    const int gx = blockIdx.x * kBG + wave * 2 + (pw >> 3);
+    const int gy = blockIdx.y * kBG + (pw & 7);
+    const int pair = blockIdx.z;
+    const bool active = gx < a.npw && gy < a.nph;
+    const int W = a.W, H = a.H;
+    const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off;
+    const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off;
+
+    if (tid == 0) {
+        bnd[0] = 0x7fffffff;
+        bnd[1] = 0x7fffffff;
+        bnd[2] = -0x7fffffff;
+        bnd[3] = -0x7fffffff;
+    }
+
+    const int irx = gx * a.steps + a.offw, iry = gy * a.steps + a.offh;
+    const float rx = (float)irx, ry = (float)iry;
+
+    // --- template gradients: Sobel (ksize 3, 1/8, reflect-101) of the level
+    // image at pixels (rx-4+c, ry-4+j), zero outside the image (zero-padded
+    // dx/dy planes, src/main.cpp:45-47). Lane q: columns q and q+4.
+    float gdx[16], gdy[16];
+    if (active) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int px = irx - 4 + q + 4 * s;
+            const bool colin = px >= 0 && px < W;
+            const int xm = clampi(reflect101(px - 1, W), 0, W - 1);
+            const int xc = clampi(px, 0, W - 1);
+            const int xp = clampi(reflect101(px + 1, W), 0, W - 1);
+            float R[10], S[10];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) {
+                const int yy = clampi(reflect101(iry - 5 + k, H), 0, H - 1);
+                const float* row = I0 + (size_t)yy * W;
+                const float l = row[xm], c = row[xc], rr = row[xp];
+                R[k] = rr - l;
+                S[k] = c * 0.25f + (l + rr) * 0.125f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int py = iry - 4 + j;
+                const bool in = colin && py >= 0 && py < H;
+                const float dx = R[j + 1] * 0.25f + (R[j] + R[j + 2]) * 0.125f;
+                const float dy = S[j + 2] - S[j];
+                gdx[8 * s + j] = in ? dx : 0.0f;
+                gdy[8 * s + j] = in ? dy : 0.0f;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) gdx[j] = gdy[j] = 0.0f;
+    }
+    LU2 lu;
+    {
+        float x[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = gdx[j] * gdx[j];
+        const float h00 = patch_sum(x);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = gdx[j] * gdy[j];
+        const float h01 = patch_sum(x);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = gdy[j] * gdy[j];
+        const float h11 = patch_sum(x);
+        lu = hessian_lu2(h00, h01, h11);
+    }
+
+    // --- initialisation from the coarser level (src/patch_grid.cpp:108-119):
+    // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
+    // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2.
+    float ix = 0.0f, iy = 0.0f;
+    if (active && a.u_coarse) {
+        const int x = (int)floorf(rx / 2), y = (int)floorf(ry / 2);
+        const int st = a.steps, hp = 4;
+        int gx0 = floordiv(x - a.c_offw - hp + st, st), gx1 = floordiv(x - a.c_offw + hp, st);
+        int gy0 = floordiv(y - a.c_offh - hp + st, st), gy1 = floordiv(y - a.c_offh + hp, st);
+        gx0 = max(gx0, 0);
+        gy0 = max(gy0, 0);
+        gx1 = min(gx1, a.c_npw - 1);
+        gy1 = min(gy1, a.c_nph - 1);
+        const float2* uc = a.u_coarse + (size_t)pair * a.u_stride;
+        float fx = 0.0f, fy = 0.0f, wt = 0.0f;
+        for (int cx = gx0; cx <= gx1; ++cx)
+            for (int cy = gy0; cy <= gy1; ++cy) {
+                const float2 v = uc[cx * a.c_nph + cy];
+                fx = fx + v.x * 0.5f;
+                fy = fy + v.y * 0.5f;
+                wt = wt + 0.5f;
+            }
+        if (wt > 0) {
+            fx = fx / wt;
+            fy = fy / wt;
+        }
+        ix = fx * 2;
+        iy = fy * 2;
+    }
+    const float sx = rx + ix, sy = ry + iy;
+    const bool valid = active && !(sx < a.tmp_lb || sy < a.tmp_lb || sx > a.tmp_ub_w || sy > a.tmp_ub_h);
+
+    // --- shared tile of the target image. Every sample position p of a patch
+    // satisfies |p - start| <= 4 (outlier test), so X = ceil(p + 1e-5f) lies in
+    // [floor(s)-4, floor(s)+6] (the epsilon is a no-op from |p| >= 256, Q8) and
+    // the taps X-5..X+3 in [floor(s)-9, floor(s)+9]; the tile takes one pixel
+    // of margin on each side: [floor(s)-10, floor(s)+10] over valid patches.
+    {
+        const int fxs = valid ? (int)floorf(sx) : 0x7fffffff;
+        const int fys = valid ? (int)floorf(sy) : 0x7fffffff;
+        const int fxl = valid ? (int)floorf(sx) : -0x7fffffff;
+        const int fyl = valid ? (int)floorf(sy) : -0x7fffffff;
+        const int m0 = wave_min(fxs), m1 = wave_min(fys), m2 = wave_max(fxl), m3 = wave_max(fyl);
+        __syncthreads();  // bnd initialised
+        if (lane == 0) {
+            atomicMin(&bnd[0], m0);
+            atomicMin(&bnd[1], m1);
+            atomicMax(&bnd[2], m2);
+            atomicMax(&bnd[3], m3);
+        }
+        __syncthreads();
+    }
+    const bool any_valid = bnd[0] != 0x7fffffff;
+    const int tx0 = bnd[0] - 10, ty0 = bnd[1] - 10;
+    const int tw = bnd[2] + 10 - tx0 + 1, th = bnd[3] + 10 - ty0 + 1;
+    const bool use_tile = any_valid && tw <= kTileMax && th <= kTileMax;
+
+    float u0 = ix, u1 = iy;
+    if (use_tile) {
+        for (int r = wave; r < th; r += 4) {
+            const float* row = I1 + (size_t)clampi(ty0 + r, 0, H - 1) * W;
+            if (lane < tw) tile[r * kTS + lane] = row[clampi(tx0 + lane, 0, W - 1)];
+        }
+        __syncthreads();
+        if (valid) {
+            iterate(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+                const float* base = tile + (w.Y - 5 - ty0) * kTS + (w.X - 5 + q - tx0);
+                return [base](int k, int c) { return base[k * kTS + c]; };
+            });
+        }
+    } else if (valid) {
+        iterate(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+            const int y0 = w.Y - 5, x0 = w.X - 5 + q;
+            return [=](int k, int c) {
+                return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
+            };
+        });
+    }
+    if (active && q == 0) a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
+}
+
+hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s)
+{
+    dim3 grid((a.npw + kBG - 1) / kBG, (a.nph + kBG - 1) / kBG, batch);
+    hipLaunchKernelGGL(k_search8, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace dis

@@ -153,3 +153,32 @@ def test_invalid_calls_fail_loudly(disflow_mod):
         eng.calc_batch(np.zeros((2, 64, 64), np.uint8), np.zeros((2, 64, 64), np.uint8))
     with pytest.raises(disflow_mod.DisError):
         eng.debug_dump(disflow_mod.STAGE_DENSE, 0)  # nothing computed yet
+
+
+@pytest.mark.parametrize("preset", ["MEDIUM", "ULTRAFAST", "SLOW"])
+def test_fast_and_generic_kernels_agree_with_oracle(disflow_mod, oracle, preset):
+    # the patch-size-8 kernel (tile + DPP reductions) against the generic one and the oracle
+    W, H = 480, 272
+    p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
+    if preset == "SLOW":
+        p.iterations = 16  # keep the CPU oracle quick
+    I0, I1 = disflow_mod.synth_pair(31, W, H)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    fast = eng.calc(I0, I1)
+    eng.set_variant(1)
+    generic = eng.calc(I0, I1)
+    _assert_bitexact(fast, generic, "fast vs generic")
+    _assert_bitexact(fast, oracle.calc_from_params(I0, I1, p), "fast vs oracle")
+
+
+def test_uncorrelated_frames_exercise_tile_fallback(disflow_mod, oracle):
+    # unrelated frames -> erratic coarse flow -> start positions spread wider
+    # than the LDS tile in many blocks (global-read fallback path)
+    W, H = 320, 256
+    I0, _ = disflow_mod.synth_pair(40, W, H)
+    _, I1 = disflow_mod.synth_pair(41, W, H)
+    I1 = np.ascontiguousarray(I1[::-1, ::-1])
+    p = disflow_mod.Params(coarsest_scale=5, finest_scale=0, patch_size=8, iterations=10,
+                           patch_overlap=0.625, patch_normalization=1)
+    got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+    _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "flow")
