@@ -65,4 +65,32 @@ __device__ __forceinline__ LU2 hessian_lu2(float h00, float h01, float h11)
     return lu2_factor(h00, h01, h10, h11);
 }
 
+// Densified flow at one level pixel (px, py) (src/patch_grid.cpp:121-182) as a
+// gather: every patch whose ps x ps footprint covers the pixel contributes
+// 0.5*u in patch-id order (gx outer, gy inner), f starts at +0, the weight is
+// the sum of the 0.5s (zero-initialised, Q7), then f /= w if w > 0.
+__device__ __forceinline__ float2 dense_at(const float2* __restrict__ u, int npw, int nph, int offw,
+                                           int offh, int steps, int hp, int px, int py)
+{
+    int gx0 = floordiv(px - offw - hp + steps, steps), gx1 = floordiv(px - offw + hp, steps);
+    int gy0 = floordiv(py - offh - hp + steps, steps), gy1 = floordiv(py - offh + hp, steps);
+    gx0 = gx0 < 0 ? 0 : gx0;
+    gy0 = gy0 < 0 ? 0 : gy0;
+    gx1 = gx1 > npw - 1 ? npw - 1 : gx1;
+    gy1 = gy1 > nph - 1 ? nph - 1 : gy1;
+    float fx = 0.0f, fy = 0.0f, w = 0.0f;
+    for (int gx = gx0; gx <= gx1; ++gx)
+        for (int gy = gy0; gy <= gy1; ++gy) {
+            const float2 v = u[gx * nph + gy];
+            fx = fx + v.x * 0.5f;
+            fy = fy + v.y * 0.5f;
+            w = w + 0.5f;
+        }
+    if (w > 0) {
+        fx = fx / w;
+        fy = fy / w;
+    }
+    return make_float2(fx, fy);
+}
+
 }  // namespace dis

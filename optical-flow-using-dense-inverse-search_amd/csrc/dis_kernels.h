@@ -56,6 +56,34 @@ struct UpsampleArgs {
     double inv_sc;
 };
 
+// Fused pyramid (dis_frontback.hip): u8 -> levels 1..`levels` (and 0 if write_l0).
+struct PyramidArgs {
+    const uint8_t* I0;
+    const uint8_t* I1;
+    size_t stride, pair_stride;
+    int W, H, Wp, Hp, pl, pt;
+    float* img0;
+    float* img1;
+    long long plane_stride;
+    int levels;    // levels produced in-kernel, 1..6 (tile = 2^levels level-0 pixels)
+    int write_l0;  // also store the level-0 magnitude plane
+    long long off[kMaxLevels];  // plane offset per level
+    int w[kMaxLevels];          // plane width per level
+};
+
+// Fused densify + upsample + crop (dis_frontback.hip).
+struct OutputArgs {
+    const float2* u;   // finest-level patch u (pre-offset)
+    float2* flow;      // W x H x 2 output, pair stride W*H
+    long long u_stride;
+    int W, H, wF, hF, F, pad_left, pad_top, xmax;
+    int npw, nph, offw, offh, steps, hp;
+    int vec_store;     // output base is 16-byte aligned and W even
+    float sc;
+};
+
+hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s);
+hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s);
 hipError_t launch_level0(const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,
                          const Geometry& g, float* img0, float* img1, int batch, hipStream_t s);
 hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int batch, hipStream_t s);

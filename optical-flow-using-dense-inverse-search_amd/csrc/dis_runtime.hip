@@ -196,6 +196,21 @@ float sqrt_threshold(float thr)
     return s;
 }
 
+// cv::resize HResizeLinear: first destination column whose source index
+// reaches wF-1; columns from there on take S[wF-1] alone (src/main.cpp:195).
+int upsample_xmax(const dis::Geometry& g)
+{
+    const int wF = g.lv[g.F].W;
+    const double inv = 1.0 / (double)std::pow(2.0f, (float)g.F);
+    for (int d = 0; d < g.Wp; ++d) {
+        const float fx = (float)((d + 0.5) * inv - 0.5);
+        int sx = (int)std::floor(fx);
+        if (sx < 0) sx = 0;
+        if (sx + 1 >= wF) return d;
+    }
+    return g.Wp;
+}
+
 // The whole path for n pairs already resident in device memory.
 dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                      size_t pair_stride, float2* flow, hipStream_t s)
@@ -204,8 +219,33 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
     const bool fast = g.ps == 8 && c->variant == 0;
     {
         TimeScope t(c, 0, s);
-        DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, c->img0, c->img1, n, s));
-        for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+        if (fast && g.C >= 1) {
+            dis::PyramidArgs pa{};
+            pa.I0 = I0;
+            pa.I1 = I1;
+            pa.stride = stride;
+            pa.pair_stride = pair_stride;
+            pa.W = g.W;
+            pa.H = g.H;
+            pa.Wp = g.Wp;
+            pa.Hp = g.Hp;
+            pa.pl = g.pad_left;
+            pa.pt = g.pad_top;
+            pa.img0 = c->img0;
+            pa.img1 = c->img1;
+            pa.plane_stride = g.plane_stride;
+            pa.levels = std::min(g.C, 6);
+            pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
+            for (int l = 0; l <= g.C; ++l) {
+                pa.off[l] = g.lv[l].plane_off;
+                pa.w[l] = g.lv[l].W;
+            }
+            DIS_HIP(dis::launch_pyramid(pa, n, s));
+            for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+        } else {
+            DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, c->img0, c->img1, n, s));
+            for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+        }
         if (!fast || c->debug)  // the fast search computes its template gradients itself
             for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, c->img0, c->dx, c->dy, n, s));
     }
@@ -273,7 +313,7 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
             TimeScope t2(c, l == g.F ? 2 : -1, s);
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s));
         }
-        if (fast && !c->debug && l != g.F) continue;  // dense flow only needed at the finest level
+        if (fast && !c->debug) continue;  // the fused output kernel densifies the finest level itself
         dis::DensifyArgs d{};
         d.u = c->pu + L.u_off;
         d.dense = c->dense + L.dense_off;
@@ -290,7 +330,31 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_densify(d, n, s));
     }
-    {
+    if (fast) {
+        const dis::LevelGeom& LF = g.lv[g.F];
+        dis::OutputArgs o{};
+        o.u = c->pu + LF.u_off;
+        o.flow = flow;
+        o.u_stride = g.u_stride;
+        o.W = g.W;
+        o.H = g.H;
+        o.wF = LF.W;
+        o.hF = LF.H;
+        o.F = g.F;
+        o.pad_left = g.pad_left;
+        o.pad_top = g.pad_top;
+        o.xmax = upsample_xmax(g);
+        o.npw = LF.npw;
+        o.nph = LF.nph;
+        o.offw = LF.offw;
+        o.offh = LF.offh;
+        o.steps = LF.steps;
+        o.hp = g.ps / 2;
+        o.vec_store = ((reinterpret_cast<uintptr_t>(flow) & 15) == 0 && (g.W & 1) == 0) ? 1 : 0;
+        o.sc = std::pow(2.0f, (float)g.F);
+        TimeScope t(c, 3, s);
+        DIS_HIP(dis::launch_output(o, n, s));
+    } else {
         const dis::LevelGeom& LF = g.lv[g.F];
         dis::UpsampleArgs u{};
         u.dense = c->dense + LF.dense_off;
@@ -305,17 +369,7 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         u.pad_top = g.pad_top;
         u.sc = std::pow(2.0f, (float)g.F);
         u.inv_sc = 1.0 / (double)u.sc;
-        // xmax: first output column whose source index reaches wF-1 (HResizeLinear)
-        u.xmax = g.Wp;
-        for (int d = 0; d < g.Wp; ++d) {
-            float fx = (float)((d + 0.5) * u.inv_sc - 0.5);
-            int sx = (int)std::floor(fx);
-            if (sx < 0) sx = 0;
-            if (sx + 1 >= LF.W) {
-                u.xmax = d;
-                break;
-            }
-        }
+        u.xmax = upsample_xmax(g);
         TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_upsample(u, n, s));
     }

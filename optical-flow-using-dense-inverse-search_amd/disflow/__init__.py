@@ -32,7 +32,7 @@ except Exception:  # pragma: no cover
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdis_hip.so")
+LIB_PATH = os.environ.get("DISFLOW_LIB") or os.path.join(_HERE, "libdis_hip.so")
 
 DIS_OK = 0
 DIS_ERR_INVALID_ARGUMENT = -1
