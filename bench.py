@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--preset", default="medium", choices=[p.name.lower() for p in disflow.Preset])
+    ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per step (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -100,6 +101,8 @@ def main():
     d1 = torch.from_numpy(I1).to(dev)
     out = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
     eng = disflow.DenseInverseSearch(params, W, H, max_batch=B, device=local)
+    if a.streams:
+        eng.set_concurrency(a.streams)
     stream = torch.cuda.current_stream(dev)
 
     def step():

@@ -139,6 +139,11 @@ typedef enum dis_stage {
 } dis_stage;
 dis_status dis_set_debug(dis_ctx* ctx, int enable);
 
+/* Concurrency: a batch call is split into `streams` sub-batches (1..8,
+ * default 2) that run on context-owned HIP streams forked from and joined
+ * back into the caller's stream. Results do not depend on this setting. */
+dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
+
 /* Kernel variant: 0 = auto (specialised kernels where available, e.g. the
  * patch_size-8 search), 1 = generic kernels only. Both are bit-identical;
  * the switch exists for parity tests and A/B timing. */

@@ -20,19 +20,21 @@ namespace dis {
 
 namespace {
 
-constexpr int kPyrT0Max = 64;                 // level-0 tile edge (2^6)
-constexpr int kPyrSS = kPyrT0Max + 2;         // u8 tile row stride (1-px halo)
 
 }  // namespace
 
-// grid: (Wp / T0, Hp / T0, 2 * batch), block 256; z = pair*2 + frame
+// grid: (Wp / T0, Hp / T0, 2 * batch), block 256; z = pair*2 + frame.
+// LEVELS (1..6) is a template parameter so every load loop has a compile-time
+// trip count and all of a thread's loads are in flight at once.
+template <int LEVELS>
 __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
 {
-    __shared__ uint8_t src[kPyrSS * kPyrSS];
-    __shared__ float buf0[(kPyrT0Max / 2) * (kPyrT0Max / 2)];
-    __shared__ float buf1[(kPyrT0Max / 4) * (kPyrT0Max / 4)];
+    constexpr int T0 = 1 << LEVELS, SS = T0 + 2, NLOAD = (SS * SS + 255) / 256;
+    constexpr int N1 = T0 / 2;
+    __shared__ uint8_t src[SS * SS];
+    __shared__ float buf0[N1 * N1];
+    __shared__ float buf1[(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
 
-    const int T0 = 1 << a.levels, SS = T0 + 2;
     const int tid = threadIdx.x;
     const int tx = blockIdx.x * T0, ty = blockIdx.y * T0;
     const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
@@ -40,19 +42,41 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
 
     // u8 tile with a 1-pixel halo: replicate padding to Wp x Hp (floor/ceil
-    // split) composed with Sobel's reflect-101 at the Wp x Hp border
-    for (int i = tid; i < SS * SS; i += 256) {
-        const int r = i / SS, c = i - r * SS;
-        const int yy = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
-        const int xx = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
-        src[i] = in[(size_t)yy * a.stride + xx];
+    // split) composed with Sobel's reflect-101 at the Wp x Hp border. Wave w
+    // loads rows w, w+4, ...; the row offset is wave-uniform (scalar unit), the
+    // column index is computed once per lane.
+    {
+        const int lane = tid & 63, wave = tid >> 6;
+        constexpr int NR = (SS + 3) / 4;  // rows per wave
+        const int c0 = lane, c1 = lane + 64;
+        const int xs0 = clampi(reflect101(tx - 1 + c0, a.Wp) - a.pl, 0, a.W - 1);
+        const int xs1 = clampi(reflect101(tx - 1 + min(c1, SS - 1), a.Wp) - a.pl, 0, a.W - 1);
+        uint8_t v0[NR], v1[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int r = wave + 4 * j;
+            const int ys = clampi(reflect101(ty - 1 + min(r, SS - 1), a.Hp) - a.pt, 0, a.H - 1);
+            const uint8_t* row = in + (size_t)__builtin_amdgcn_readfirstlane(ys) * a.stride;
+            v0[j] = (c0 < SS) ? row[xs0] : 0;
+            v1[j] = (c1 < SS) ? row[xs1] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int r = wave + 4 * j;
+            if (r < SS) {
+                if (c0 < SS) src[r * SS + c0] = v0[j];
+                if (c1 < SS) src[r * SS + c1] = v1[j];
+            }
+        }
     }
     __syncthreads();
 
     // level 1 (and level 0 when requested)
-    const int n1 = T0 / 2;
-    for (int k = tid; k < n1 * n1; k += 256) {
-        const int y1 = k / n1, x1 = k - y1 * n1;
+#pragma unroll
+    for (int k0 = 0; k0 < N1 * N1; k0 += 256) {
+        const int k = k0 + tid;
+        if (N1 * N1 % 256 != 0 && k >= N1 * N1) break;
+        const int y1 = k / N1, x1 = k - y1 * N1;
         float v[4][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -91,10 +115,11 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
         planes[a.off[1] + (size_t)(ty / 2 + y1) * a.w[1] + tx / 2 + x1] = l1;
     }
 
-    // levels 2..levels from LDS, ping-pong buf0 <-> buf1
+    // levels 2..LEVELS from LDS, ping-pong buf0 <-> buf1
     float* cur = buf0;
     float* nxt = buf1;
-    for (int l = 2; l <= a.levels; ++l) {
+#pragma unroll
+    for (int l = 2; l <= LEVELS; ++l) {
         __syncthreads();
         const int ns = T0 >> (l - 1), nd = ns / 2;
         for (int k = tid; k < nd * nd; k += 256) {
@@ -116,9 +141,16 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s)
 {
     const int T0 = 1 << a.levels;
-    if (a.levels < 1 || T0 > kPyrT0Max || a.Wp % T0 || a.Hp % T0) return hipErrorInvalidValue;
+    if (a.levels < 1 || a.levels > 6 || a.Wp % T0 || a.Hp % T0) return hipErrorInvalidValue;
     dim3 grid(a.Wp / T0, a.Hp / T0, 2 * batch);
-    hipLaunchKernelGGL(k_pyramid, grid, dim3(256), 0, s, a);
+    switch (a.levels) {
+        case 1: hipLaunchKernelGGL(k_pyramid<1>, grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_pyramid<2>, grid, dim3(256), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_pyramid<3>, grid, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_pyramid<4>, grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(k_pyramid<5>, grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_pyramid<6>, grid, dim3(256), 0, s, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -128,8 +160,9 @@ hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s)
 namespace {
 
 constexpr int kOutTW = 64, kOutTH = 16;  // full-resolution output tile per workgroup
-constexpr int kOutSW = kOutTW / 2 + 3;   // level-F source tile bound (F >= 1)
-constexpr int kOutSH = kOutTH / 2 + 3;
+constexpr int kOutSW = kOutTW + 3;       // level-F dense window bound (F == 0 is the widest)
+constexpr int kOutSH = kOutTH + 3;
+constexpr int kOutPX = 48, kOutPY = 32;  // staged patch block (grid columns x rows)
 
 // cv::resize INTER_LINEAR source index / fraction for destination index d at
 // scale 2^F: s = (d + .5) * 2^-F - .5 (exact dyadic in float), clamped.
@@ -152,41 +185,85 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 
 }  // namespace
 
-// F == 0: crop of the densified level-0 flow. grid (ceil(W/64), ceil(H/4), batch)
-__global__ void __launch_bounds__(256) k_output0(OutputArgs a)
-{
-    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
-    const int pair = blockIdx.z;
-    if (x >= a.W || y >= a.H) return;
-    const float2* u = a.u + (size_t)pair * a.u_stride;
-    a.flow[(size_t)pair * a.W * a.H + (size_t)y * a.W + x] =
-        dense_at(u, a.npw, a.nph, a.offw, a.offh, a.steps, a.hp, x + a.pad_left, y + a.pad_top);
-}
-
-// F >= 1: grid (ceil(W/64), ceil(H/16), batch), block 256 (2x2 pixels per thread)
+// grid (ceil(W/64), ceil(H/16), batch), block 256 (2x2 output pixels per thread).
+// 1) stage the patch displacements covering this tile's level-F window in LDS
+//    (one round of loads), 2) densify the window into LDS (src/patch_grid.cpp:
+//    121-182), 3) F == 0: crop; F >= 1: scale by 2^F, resize, crop.
+template <bool UPSAMPLE>
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
+    __shared__ float2 pu[kOutPX * kOutPY];
     __shared__ float2 dense[kOutSW * kOutSH];
+    __shared__ int2 cr[kOutSW], rr[kOutSH];
     const int tid = threadIdx.x;
     const int ox = blockIdx.x * kOutTW, oy = blockIdx.y * kOutTH;
     const int pair = blockIdx.z;
     const float2* u = a.u + (size_t)pair * a.u_stride;
-    const float sc = a.sc;
 
-    // source window of this tile at level F
+    // level-F window of this tile
     int i0, i1, j0, j1;
-    float f;
-    lin_coef(ox + a.pad_left, a.wF, a.F, &i0, &f);
-    lin_coef(min(ox + kOutTW - 1, a.W - 1) + a.pad_left, a.wF, a.F, &i1, &f);
-    lin_coef(oy + a.pad_top, a.hF, a.F, &j0, &f);
-    lin_coef(min(oy + kOutTH - 1, a.H - 1) + a.pad_top, a.hF, a.F, &j1, &f);
-    i1 = min(i1 + 1, a.wF - 1);
-    j1 = min(j1 + 1, a.hF - 1);
+    if (UPSAMPLE) {
+        float f;
+        lin_coef(ox + a.pad_left, a.wF, a.F, &i0, &f);
+        lin_coef(min(ox + kOutTW - 1, a.W - 1) + a.pad_left, a.wF, a.F, &i1, &f);
+        lin_coef(oy + a.pad_top, a.hF, a.F, &j0, &f);
+        lin_coef(min(oy + kOutTH - 1, a.H - 1) + a.pad_top, a.hF, a.F, &j1, &f);
+        i1 = min(i1 + 1, a.wF - 1);
+        j1 = min(j1 + 1, a.hF - 1);
+    } else {
+        i0 = ox + a.pad_left;
+        j0 = oy + a.pad_top;
+        i1 = min(ox + kOutTW - 1, a.W - 1) + a.pad_left;
+        j1 = min(oy + kOutTH - 1, a.H - 1) + a.pad_top;
+    }
     const int rw = i1 - i0 + 1, rh = j1 - j0 + 1;
+    // patches whose footprint meets the window
+    const int st = a.steps, hp = a.hp;
+    const int ga = max(0, floordiv(i0 - a.offw - hp + st, st)), gb = min(a.npw - 1, floordiv(i1 - a.offw + hp, st));
+    const int ha = max(0, floordiv(j0 - a.offh - hp + st, st)), hb = min(a.nph - 1, floordiv(j1 - a.offh + hp, st));
+    const int PW = gb - ga + 1, PH = hb - ha + 1;  // <= kOutPX x kOutPY (output_fits)
+    {
+        constexpr int NL = kOutPX * kOutPY / 256;
+        float2 v[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int k = tid + 256 * j;
+            const int cx = k / kOutPY, cy = k % kOutPY;
+            v[j] = (cx < PW && cy < PH) ? u[(ga + cx) * a.nph + ha + cy] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) pu[tid + 256 * j] = v[j];
+    }
+    // covering patch ranges per window column / row (one floordiv pair each)
+    if (tid < rw) {
+        const int px = i0 + tid;
+        cr[tid] = make_int2(max(floordiv(px - a.offw - hp + st, st), ga) - ga,
+                            min(floordiv(px - a.offw + hp, st), gb) - ga);
+    } else if (tid >= 128 && tid - 128 < rh) {
+        const int py = j0 + tid - 128;
+        rr[tid - 128] = make_int2(max(floordiv(py - a.offh - hp + st, st), ha) - ha,
+                                  min(floordiv(py - a.offh + hp, st), hb) - ha);
+    }
+    __syncthreads();
+    const float sc = a.sc;
     for (int k = tid; k < rw * rh; k += 256) {
         const int r = k / rw, c = k - r * rw;
-        const float2 d = dense_at(u, a.npw, a.nph, a.offw, a.offh, a.steps, a.hp, i0 + c, j0 + r);
-        dense[r * kOutSW + c] = make_float2(d.x * sc, d.y * sc);  // flowout *= sc_fct (:194)
+        // dense_at() over the staged displacements: patch-id order, f from +0
+        const int2 xr = cr[c], yr = rr[r];
+        float fx = 0.0f, fy = 0.0f, w = 0.0f;
+        for (int gx = xr.x; gx <= xr.y; ++gx)
+            for (int gy = yr.x; gy <= yr.y; ++gy) {
+                const float2 t = pu[gx * kOutPY + gy];
+                fx = fx + t.x * 0.5f;
+                fy = fy + t.y * 0.5f;
+                w = w + 0.5f;
+            }
+        if (w > 0) {
+            fx = fx / w;
+            fy = fy / w;
+        }
+        // flowout *= sc_fct (src/main.cpp:194) before the resize
+        dense[r * kOutSW + c] = UPSAMPLE ? make_float2(fx * sc, fy * sc) : make_float2(fx, fy);
     }
     __syncthreads();
 
@@ -195,35 +272,41 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     for (int dy = 0; dy < 2; ++dy) {
         const int y = py + dy;
         if (y >= a.H) continue;
-        int yi;
-        float yf;
-        lin_coef(y + a.pad_top, a.hF, a.F, &yi, &yf);
-        const int r0 = yi - j0, r1 = min(yi + 1, a.hF - 1) - j0;
-        const float b0 = 1.f - yf, b1 = yf;
         float2 o[2];
+        if (UPSAMPLE) {
+            int yi;
+            float yf;
+            lin_coef(y + a.pad_top, a.hF, a.F, &yi, &yf);
+            const int r0 = yi - j0, r1 = min(yi + 1, a.hF - 1) - j0;
+            const float b0 = 1.f - yf, b1 = yf;
 #pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-            const int xx = px + dx + a.pad_left;
-            int xi;
-            float xf;
-            lin_coef(xx, a.wF, a.F, &xi, &xf);
-            const bool two = xx < a.xmax;
-            const int c0 = xi - i0;
-            float h[2][2];
+            for (int dx = 0; dx < 2; ++dx) {
+                const int xx = px + dx + a.pad_left;
+                int xi;
+                float xf;
+                lin_coef(xx, a.wF, a.F, &xi, &xf);
+                const bool two = xx < a.xmax;
+                const int c0 = xi - i0;
+                float h[2][2];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const float2* row = dense + (k ? r1 : r0) * kOutSW;
-                const float2 s0 = row[c0];
-                if (two) {
-                    const float2 s1 = row[c0 + 1];
-                    h[k][0] = s0.x * (1.f - xf) + s1.x * xf;
-                    h[k][1] = s0.y * (1.f - xf) + s1.y * xf;
-                } else {
-                    h[k][0] = s0.x;
-                    h[k][1] = s0.y;
+                for (int k = 0; k < 2; ++k) {
+                    const float2* row = dense + (k ? r1 : r0) * kOutSW;
+                    const float2 s0 = row[c0];
+                    if (two) {
+                        const float2 s1 = row[c0 + 1];
+                        h[k][0] = s0.x * (1.f - xf) + s1.x * xf;
+                        h[k][1] = s0.y * (1.f - xf) + s1.y * xf;
+                    } else {
+                        h[k][0] = s0.x;
+                        h[k][1] = s0.y;
+                    }
                 }
+                o[dx] = make_float2(h[0][0] * b0 + h[1][0] * b1, h[0][1] * b0 + h[1][1] * b1);
             }
-            o[dx] = make_float2(h[0][0] * b0 + h[1][0] * b1, h[0][1] * b0 + h[1][1] * b1);
+        } else {
+            const float2* row = dense + (y - oy) * kOutSW + (px - ox);
+            o[0] = row[0];
+            o[1] = row[1];
         }
         float2* dst = a.flow + (size_t)pair * a.W * a.H + (size_t)y * a.W + px;
         if (px + 1 < a.W) {
@@ -239,16 +322,21 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     }
 }
 
+bool output_fits(const OutputArgs& a)
+{
+    // the staged patch block must fit: (window + ps) / steps + 1 per axis
+    const int pw = (kOutSW + 2 * a.hp) / a.steps + 2, ph = (kOutSH + 2 * a.hp) / a.steps + 2;
+    return pw <= kOutPX && ph <= kOutPY;
+}
+
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s)
 {
-    if (a.F == 0) {
-        hipLaunchKernelGGL(k_output0, dim3((a.W + 63) / 64, (a.H + 3) / 4, batch), dim3(64, 4), 0, s, a);
-    } else {
-        // the level-F window of a 64 x 16 output tile must fit the LDS tile
-        if ((kOutTW >> a.F) + 3 > kOutSW || (kOutTH >> a.F) + 3 > kOutSH) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_output, dim3((a.W + kOutTW - 1) / kOutTW, (a.H + kOutTH - 1) / kOutTH, batch),
-                           dim3(256), 0, s, a);
-    }
+    if (!output_fits(a)) return hipErrorInvalidValue;
+    dim3 grid((a.W + kOutTW - 1) / kOutTW, (a.H + kOutTH - 1) / kOutTH, batch);
+    if (a.F == 0)
+        hipLaunchKernelGGL(k_output<false>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_output<true>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ struct Search8Args {
     float tmp_lb, tmp_ub_w, tmp_ub_h;
     float thr_sq;             // largest float s with sqrtf(s) <= outlierthresh
     int iters, norm;
+    int tile_stride;          // LDS tile row stride (search8_tile_stride(steps))
 };
 
 struct DensifyArgs {
@@ -83,6 +84,7 @@ struct OutputArgs {
 };
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s);
+bool output_fits(const OutputArgs& a);
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s);
 hipError_t launch_level0(const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,
                          const Geometry& g, float* img0, float* img1, int batch, hipStream_t s);
@@ -90,6 +92,7 @@ hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int 
 hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, float* dy, int batch,
                         hipStream_t s);
 hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s);
+int search8_tile_stride(int steps);
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s);
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);

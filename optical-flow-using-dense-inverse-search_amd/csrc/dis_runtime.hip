@@ -101,6 +101,11 @@ struct dis_ctx {
     int variant = 0;  // 0 auto (fast kernels where available), 1 generic only
     int last_batch = 0;
     hipStream_t own = nullptr;
+    static constexpr int kMaxSub = 8;
+    int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
+    hipStream_t sub[kMaxSub] = {};
+    hipEvent_t fork = nullptr;
+    hipEvent_t join[kMaxSub] = {};
     // workspace (device)
     float* img0 = nullptr;
     float* img1 = nullptr;
@@ -212,10 +217,17 @@ int upsample_xmax(const dis::Geometry& g)
 }
 
 // The whole path for n pairs already resident in device memory.
-dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
+dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
                      size_t pair_stride, float2* flow, hipStream_t s)
 {
     const dis::Geometry& g = c->g;
+    // this sub-batch's slice of the workspace (pairs p0 .. p0+n-1)
+    float* const img0 = c->img0 + (size_t)p0 * g.plane_stride;
+    float* const img1 = c->img1 + (size_t)p0 * g.plane_stride;
+    float* const gdx = c->dx + (size_t)p0 * g.plane_stride;
+    float* const gdy = c->dy + (size_t)p0 * g.plane_stride;
+    float2* const pu = c->pu + (size_t)p0 * g.u_stride;
+    float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant == 0;
     {
         TimeScope t(c, 0, s);
@@ -231,8 +243,8 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
             pa.Hp = g.Hp;
             pa.pl = g.pad_left;
             pa.pt = g.pad_top;
-            pa.img0 = c->img0;
-            pa.img1 = c->img1;
+            pa.img0 = img0;
+            pa.img1 = img1;
             pa.plane_stride = g.plane_stride;
             pa.levels = std::min(g.C, 6);
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
@@ -241,23 +253,23 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
                 pa.w[l] = g.lv[l].W;
             }
             DIS_HIP(dis::launch_pyramid(pa, n, s));
-            for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+            for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         } else {
-            DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, c->img0, c->img1, n, s));
-            for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, c->img0, c->img1, n, s));
+            DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
+            for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }
         if (!fast || c->debug)  // the fast search computes its template gradients itself
-            for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, c->img0, c->dx, c->dy, n, s));
+            for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, img0, gdx, gdy, n, s));
     }
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         const dis::LevelGeom& L = g.lv[l];
         dis::SearchArgs a{};
-        a.img0 = c->img0;
-        a.img1 = c->img1;
-        a.dx = c->dx;
-        a.dy = c->dy;
-        a.dense_coarse = (l < g.C) ? c->dense + g.lv[l + 1].dense_off : nullptr;
-        a.u_out = c->pu + L.u_off;
+        a.img0 = img0;
+        a.img1 = img1;
+        a.dx = gdx;
+        a.dy = gdy;
+        a.dense_coarse = (l < g.C) ? dense + g.lv[l + 1].dense_off : nullptr;
+        a.u_out = pu + L.u_off;
         a.plane_stride = g.plane_stride;
         a.plane_off = L.plane_off;
         a.dense_stride = g.dense_stride;
@@ -279,10 +291,10 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         a.norm = g.norm;
         if (fast) {
             dis::Search8Args b{};
-            b.img0 = c->img0;
-            b.img1 = c->img1;
-            b.u_coarse = (l < g.C) ? c->pu + g.lv[l + 1].u_off : nullptr;
-            b.u_out = c->pu + L.u_off;
+            b.img0 = img0;
+            b.img1 = img1;
+            b.u_coarse = (l < g.C) ? pu + g.lv[l + 1].u_off : nullptr;
+            b.u_out = pu + L.u_off;
             b.plane_stride = g.plane_stride;
             b.plane_off = L.plane_off;
             b.u_stride = g.u_stride;
@@ -303,6 +315,7 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
             b.tmp_ub_w = L.tmp_ub_w;
             b.tmp_ub_h = L.tmp_ub_h;
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
+            b.tile_stride = dis::search8_tile_stride(L.steps);
             b.iters = g.iters;
             b.norm = g.norm;
             TimeScope t1(c, 1, s);
@@ -315,8 +328,8 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         }
         if (fast && !c->debug) continue;  // the fused output kernel densifies the finest level itself
         dis::DensifyArgs d{};
-        d.u = c->pu + L.u_off;
-        d.dense = c->dense + L.dense_off;
+        d.u = pu + L.u_off;
+        d.dense = dense + L.dense_off;
         d.u_stride = g.u_stride;
         d.dense_stride = g.dense_stride;
         d.W = L.W;
@@ -330,10 +343,11 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_densify(d, n, s));
     }
+    dis::OutputArgs o{};
+    bool fused_out = false;
     if (fast) {
         const dis::LevelGeom& LF = g.lv[g.F];
-        dis::OutputArgs o{};
-        o.u = c->pu + LF.u_off;
+        o.u = pu + LF.u_off;
         o.flow = flow;
         o.u_stride = g.u_stride;
         o.W = g.W;
@@ -352,12 +366,33 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         o.hp = g.ps / 2;
         o.vec_store = ((reinterpret_cast<uintptr_t>(flow) & 15) == 0 && (g.W & 1) == 0) ? 1 : 0;
         o.sc = std::pow(2.0f, (float)g.F);
+        fused_out = dis::output_fits(o);
+    }
+    if (fused_out) {
         TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_output(o, n, s));
     } else {
+        if (fast && !c->debug) {  // the search loop skipped the finest densify: do it here
+            const dis::LevelGeom& L = g.lv[g.F];
+            dis::DensifyArgs d{};
+            d.u = pu + L.u_off;
+            d.dense = dense + L.dense_off;
+            d.u_stride = g.u_stride;
+            d.dense_stride = g.dense_stride;
+            d.W = L.W;
+            d.H = L.H;
+            d.ps = g.ps;
+            d.steps = L.steps;
+            d.npw = L.npw;
+            d.nph = L.nph;
+            d.offw = L.offw;
+            d.offh = L.offh;
+            TimeScope t(c, 3, s);
+            DIS_HIP(dis::launch_densify(d, n, s));
+        }
         const dis::LevelGeom& LF = g.lv[g.F];
         dis::UpsampleArgs u{};
-        u.dense = c->dense + LF.dense_off;
+        u.dense = dense + LF.dense_off;
         u.flow = flow;
         u.dense_stride = g.dense_stride;
         u.W = g.W;
@@ -373,6 +408,32 @@ dis_status run_batch(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, si
         TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_upsample(u, n, s));
     }
+    return DIS_OK;
+}
+
+// Split n pairs into sub-batches on the context's streams (fork from `s`,
+// join back into `s`): pairs are independent, so the latency-bound phases of
+// one sub-batch (coarse levels, kernel tails) overlap the others' work.
+dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                       size_t pair_stride, float2* flow, hipStream_t s)
+{
+    const int S = std::min(c->nsub, n);
+    if (S <= 1) {
+        dis_status st = run_batch(c, n, 0, I0, I1, stride, pair_stride, flow, s);
+        if (st == DIS_OK) c->last_batch = n;
+        return st;
+    }
+    DIS_HIP(hipEventRecord(c->fork, s));
+    const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
+    for (int k = 0; k < S; ++k) {
+        const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
+        DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+        dis_status st = run_batch(c, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride, stride,
+                                  pair_stride, flow + (size_t)a * fpp, c->sub[k]);
+        if (st != DIS_OK) return st;
+        DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
+    }
+    for (int k = 0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     c->last_batch = n;
     return DIS_OK;
 }
@@ -497,7 +558,11 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->in0, (size_t)width * height * B) == hipSuccess &&
               hipMalloc(&c->in1, (size_t)width * height * B) == hipSuccess &&
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess;
+              hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; ok && k < dis_ctx::kMaxSub; ++k)
+        ok = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         free_ws(c);
         if (c->own) hipStreamDestroy(c->own);
@@ -515,6 +580,12 @@ dis_status dis_destroy(dis_ctx* c)
     if (c->own) hipStreamSynchronize(c->own);
     free_ws(c);
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
+    for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+        if (c->sub[k]) hipStreamSynchronize(c->sub[k]);
+        if (c->sub[k]) hipStreamDestroy(c->sub[k]);
+        if (c->join[k]) hipEventDestroy(c->join[k]);
+    }
+    if (c->fork) hipEventDestroy(c->fork);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return DIS_OK;
@@ -533,7 +604,7 @@ dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     if (n > 1 && pair_stride < stride * H) return fail(DIS_ERR_INVALID_ARGUMENT, "pair_stride too small");
     DIS_HIP(hipSetDevice(c->device));
     if (where == DIS_MEM_DEVICE) {
-        return run_batch(c, n, I0, I1, stride, pair_stride, reinterpret_cast<float2*>(flow),
+        return run_batches(c, n, I0, I1, stride, pair_stride, reinterpret_cast<float2*>(flow),
                          reinterpret_cast<hipStream_t>(stream));
     }
     if (where != DIS_MEM_HOST) return fail(DIS_ERR_INVALID_ARGUMENT, "bad dis_mem");
@@ -545,7 +616,7 @@ dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         DIS_HIP(hipMemcpy2DAsync(c->in1 + k * fsz, W, I1 + k * pair_stride, stride, W, H,
                                  hipMemcpyHostToDevice, s));
     }
-    dis_status st = run_batch(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
+    dis_status st = run_batches(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
     if (st != DIS_OK) return st;
     DIS_HIP(hipMemcpyAsync(flow, c->out, sizeof(float2) * fsz * n, hipMemcpyDeviceToHost, s));
     DIS_HIP(hipStreamSynchronize(s));
@@ -562,6 +633,15 @@ dis_status dis_set_debug(dis_ctx* c, int enable)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
     c->debug = enable ? 1 : 0;  // this build always materialises every stage
+    return DIS_OK;
+}
+
+dis_status dis_set_concurrency(dis_ctx* c, int streams)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (streams < 1 || streams > dis_ctx::kMaxSub)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "streams must be in [1, 8]");
+    c->nsub = streams;
     return DIS_OK;
 }
 

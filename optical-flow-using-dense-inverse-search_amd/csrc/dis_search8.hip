@@ -22,13 +22,17 @@
 #include "dis_device.h"
 #include "dis_kernels.h"
 
+#ifndef DIS_SEARCH8_WAVES
+#define DIS_SEARCH8_WAVES 4  // min waves per SIMD (caps VGPRs at 128)
+#endif
+
 namespace dis {
 
 namespace {
 
 constexpr int kBG = 8;             // patch-grid block per workgroup: kBG x kBG patches
 constexpr int kTileMax = 64;       // max staged tile edge (pixels)
-constexpr int kTS = kTileMax + 1;  // tile row stride (floats): odd -> fewer bank conflicts
+constexpr int kTSMax = 96;         // max tile row stride (floats); the host picks it per grid step
 
 // quad_perm DPP controls
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
@@ -168,9 +172,10 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 }  // namespace
 
 // grid: (ceil(npw/8), ceil(nph/8), batch); block 256
-__global__ void __launch_bounds__(256) k_search8(Search8Args a)
+__global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args a)
 {
-    __shared__ float tile[kTileMax * kTS];
+    __shared__ float tile[kTileMax * kTSMax];
+    __shared__ float2 cu[256];
     __shared__ int bnd[4];
 
     const int tid = threadIdx.x;
@@ -247,31 +252,45 @@ __global__ void __launch_bounds__(256) k_search8(Search8Args a)
     // --- initialisation from the coarser level (src/patch_grid.cpp:108-119):
     // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
     // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2.
+    // The coarse patches any patch of this block needs are staged in LDS first
+    // (one load per thread), so the gathers below are LDS reads.
     float ix = 0.0f, iy = 0.0f;
-    if (active && a.u_coarse) {
-        const int x = (int)floorf(rx / 2), y = (int)floorf(ry / 2);
+    if (a.u_coarse) {
         const int st = a.steps, hp = 4;
-        int gx0 = floordiv(x - a.c_offw - hp + st, st), gx1 = floordiv(x - a.c_offw + hp, st);
-        int gy0 = floordiv(y - a.c_offh - hp + st, st), gy1 = floordiv(y - a.c_offh + hp, st);
-        gx0 = max(gx0, 0);
-        gy0 = max(gy0, 0);
-        gx1 = min(gx1, a.c_npw - 1);
-        gy1 = min(gy1, a.c_nph - 1);
+        const int bgx0 = blockIdx.x * kBG, bgx1 = min(bgx0 + kBG - 1, a.npw - 1);
+        const int bgy0 = blockIdx.y * kBG, bgy1 = min(bgy0 + kBG - 1, a.nph - 1);
+        const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
+        const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
+        const int ga = max(0, floordiv(xlo - a.c_offw - hp + st, st));
+        const int gb = min(a.c_npw - 1, floordiv(xhi - a.c_offw + hp, st));
+        const int ha = max(0, floordiv(ylo - a.c_offh - hp + st, st));
+        const int hb = min(a.c_nph - 1, floordiv(yhi - a.c_offh + hp, st));
+        const int PH = hb - ha + 1, PN = (gb - ga + 1) * PH;  // <= 12 x 12 (host-checked)
         const float2* uc = a.u_coarse + (size_t)pair * a.u_stride;
-        float fx = 0.0f, fy = 0.0f, wt = 0.0f;
-        for (int cx = gx0; cx <= gx1; ++cx)
-            for (int cy = gy0; cy <= gy1; ++cy) {
-                const float2 v = uc[cx * a.c_nph + cy];
-                fx = fx + v.x * 0.5f;
-                fy = fy + v.y * 0.5f;
-                wt = wt + 0.5f;
-            }
-        if (wt > 0) {
-            fx = fx / wt;
-            fy = fy / wt;
+        if (tid < PN) {
+            const int cx = tid / PH, cy = tid - cx * PH;
+            cu[tid] = uc[(ga + cx) * a.c_nph + ha + cy];
         }
-        ix = fx * 2;
-        iy = fy * 2;
+        __syncthreads();
+        if (active) {
+            const int x = (int)floorf(rx / 2), y = (int)floorf(ry / 2);
+            const int gx0 = max(floordiv(x - a.c_offw - hp + st, st), ga), gx1 = min(floordiv(x - a.c_offw + hp, st), gb);
+            const int gy0 = max(floordiv(y - a.c_offh - hp + st, st), ha), gy1 = min(floordiv(y - a.c_offh + hp, st), hb);
+            float fx = 0.0f, fy = 0.0f, wt = 0.0f;
+            for (int cx = gx0; cx <= gx1; ++cx)
+                for (int cy = gy0; cy <= gy1; ++cy) {
+                    const float2 v = cu[(cx - ga) * PH + cy - ha];
+                    fx = fx + v.x * 0.5f;
+                    fy = fy + v.y * 0.5f;
+                    wt = wt + 0.5f;
+                }
+            if (wt > 0) {
+                fx = fx / wt;
+                fy = fy / wt;
+            }
+            ix = fx * 2;
+            iy = fy * 2;
+        }
     }
     const float sx = rx + ix, sy = ry + iy;
     const bool valid = active && !(sx < a.tmp_lb || sy < a.tmp_lb || sx > a.tmp_ub_w || sy > a.tmp_ub_h);
@@ -300,18 +319,28 @@ __global__ void __launch_bounds__(256) k_search8(Search8Args a)
     const int tx0 = bnd[0] - 10, ty0 = bnd[1] - 10;
     const int tw = bnd[2] + 10 - tx0 + 1, th = bnd[3] + 10 - ty0 + 1;
     const bool use_tile = any_valid && tw <= kTileMax && th <= kTileMax;
+    const int TS = a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
 
     float u0 = ix, u1 = iy;
     if (use_tile) {
-        for (int r = wave; r < th; r += 4) {
-            const float* row = I1 + (size_t)clampi(ty0 + r, 0, H - 1) * W;
-            if (lane < tw) tile[r * kTS + lane] = row[clampi(tx0 + lane, 0, W - 1)];
+        // all of this wave's rows in flight at once, then the LDS stores
+        float v[kTileMax / 4];
+        const int cx = clampi(tx0 + lane, 0, W - 1);
+#pragma unroll
+        for (int j = 0; j < kTileMax / 4; ++j) {
+            const int r = wave + 4 * j;
+            v[j] = (r < th && lane < tw) ? I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + cx] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < kTileMax / 4; ++j) {
+            const int r = wave + 4 * j;
+            if (r < th && lane < tw) tile[r * TS + lane] = v[j];
         }
         __syncthreads();
         if (valid) {
             iterate(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
-                const float* base = tile + (w.Y - 5 - ty0) * kTS + (w.X - 5 + q - tx0);
-                return [base](int k, int c) { return base[k * kTS + c]; };
+                const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + q - tx0);
+                return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
         }
     } else if (valid) {
@@ -325,8 +354,31 @@ __global__ void __launch_bounds__(256) k_search8(Search8Args a)
     if (active && q == 0) a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
 }
 
+// LDS tile row stride for grid step `steps`: the 8 vertically adjacent patches
+// of a half-wave (4 lanes each) sit steps*S floats apart; pick S in
+// [kTileMax+1, kTSMax] minimising the worst bank multiplicity of
+// (steps*S*g + q) mod 32, g < 8, q < 4 (ds_read_b32 banking, 32-lane groups).
+int search8_tile_stride(int steps)
+{
+    int best = kTileMax + 1, best_m = 1 << 30;
+    for (int S = kTileMax + 1; S <= kTSMax; ++S) {
+        int cnt[32] = {0}, m = 0;
+        for (int g = 0; g < 8; ++g)
+            for (int q = 0; q < 4; ++q) {
+                const int b = (int)(((long long)steps * S * g + q) % 32);
+                m = ++cnt[b] > m ? cnt[b] : m;
+            }
+        if (m < best_m) {
+            best_m = m;
+            best = S;
+        }
+    }
+    return best;
+}
+
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s)
 {
+    if (a.tile_stride < kTileMax + 1 || a.tile_stride > kTSMax) return hipErrorInvalidValue;
     dim3 grid((a.npw + kBG - 1) / kBG, (a.nph + kBG - 1) / kBG, batch);
     hipLaunchKernelGGL(k_search8, grid, dim3(256), 0, s, a);
     return hipGetLastError();

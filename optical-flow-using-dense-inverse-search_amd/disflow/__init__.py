@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     "dis_workload_info", "dis_create", "dis_destroy", "dis_calc_u8", "dis_calc_batch_u8",
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
+    "dis_set_concurrency",
 )
 
 
@@ -140,6 +141,7 @@ def lib() -> ctypes.CDLL:
         L.dis_flow_from_pyramids.argtypes = [P(V)] * 6 + [I, V, I, I, I, I, I, I, F, I, I]
         L.dis_set_debug.argtypes = [V, I]
         L.dis_set_kernel_variant.argtypes = [V, I]
+        L.dis_set_concurrency.argtypes = [V, I]
         L.dis_stage_size.argtypes = [V, I, I, P(Z)]
         L.dis_debug_dump.argtypes = [V, I, I, I, V, Z]
         L.dis_set_kernel_timing.argtypes = [V, I]
@@ -233,6 +235,10 @@ class DenseInverseSearch:
     def set_variant(self, variant: int) -> None:
         """0 = specialised kernels where available, 1 = generic kernels only."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
+
+    def set_concurrency(self, streams: int) -> None:
+        """Sub-batch streams per calc (1..8); results are identical for any value."""
+        _check(lib().dis_set_concurrency(self._ctx, streams))
 
     def set_debug(self, on: bool = True) -> None:
         _check(lib().dis_set_debug(self._ctx, int(on)))

@@ -110,6 +110,10 @@ def test_batch_equals_single_and_deterministic(disflow_mod):
     batch = eng.calc_batch(I0, I1)
     again = eng.calc_batch(I0, I1)
     assert np.array_equal(batch.view(np.uint32), again.view(np.uint32))
+    for streams in (1, 3, 8):
+        eng.set_concurrency(streams)
+        other = eng.calc_batch(I0, I1)
+        assert np.array_equal(other.view(np.uint32), batch.view(np.uint32)), streams
     single = disflow_mod.DenseInverseSearch(p, W, H)
     for k in range(4):
         one = single.calc(I0[k], I1[k])
@@ -182,3 +186,15 @@ def test_uncorrelated_frames_exercise_tile_fallback(disflow_mod, oracle):
                            patch_overlap=0.625, patch_normalization=1)
     got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
     _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "flow")
+
+
+def test_dense_grid_overlap_fallbacks(disflow_mod, oracle):
+    # steps = 1 (overlap 0.9): the fused output kernel's patch staging does not
+    # fit, so the densify + upsample kernels run instead; F = 1 and F = 0
+    W, H = 96, 80
+    I0, I1 = disflow_mod.synth_pair(50, W, H)
+    for F in (1, 0):
+        p = disflow_mod.Params(coarsest_scale=3, finest_scale=F, patch_size=8, iterations=4,
+                               patch_overlap=0.9, patch_normalization=1)
+        got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+        _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), f"flow F={F}")
