@@ -198,3 +198,14 @@ def test_dense_grid_overlap_fallbacks(disflow_mod, oracle):
                                patch_overlap=0.9, patch_normalization=1)
         got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
         _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), f"flow F={F}")
+
+
+@pytest.mark.parametrize("name", sorted(f for f in __import__("os").listdir(helpers.GOLDEN) if f.endswith(".npz")))
+def test_golden_fixtures_on_gpu(disflow_mod, name):
+    import os
+    z = np.load(os.path.join(helpers.GOLDEN, name))
+    C, F, ps, it, norm = (int(v) for v in z["knobs_i"])
+    H, W = z["I0"].shape
+    p = _params(disflow_mod, C, F, ps, it, float(z["knobs_f"][0]), norm)
+    got = disflow_mod.DenseInverseSearch(p, W, H).calc(z["I0"], z["I1"])
+    _assert_bitexact(got, z["flow"], name)

@@ -1,0 +1,106 @@
+"""Multi-rank sharding of frame pairs (disflow.multi): world_size-2 gloo runs on
+CPU with a deterministic stand-in compute (the real kernels need a GPU), and a
+GPU run where two processes share the one card of the test box and must
+reproduce the single-process flows bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import disflow.multi as multi
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _fake_compute(I0, I1):
+    # deterministic per-pair stand-in for the GPU path (no cross-pair state)
+    d = I1.astype(np.float32) - I0.astype(np.float32)
+    return np.stack([d, d * 0.5], axis=-1)
+
+
+def _pairs(n, H=12, W=16, seed=3):
+    rng = np.random.default_rng(seed)
+    return (rng.integers(0, 256, (n, H, W), dtype=np.uint8), rng.integers(0, 256, (n, H, W), dtype=np.uint8))
+
+
+def test_shard_bounds_cover_exactly():
+    for n in (0, 1, 7, 32, 256):
+        for world in (1, 2, 3, 8):
+            got = [multi.shard_bounds(n, r, world) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(got[i][1] == got[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in got]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        multi.shard_bounds(4, 2, 2)
+
+
+def _worker(rank, world, port, n, out_q, use_gpu):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        I0, I1 = _pairs(n) if not use_gpu else _gpu_pairs(n)
+        if use_gpu:
+            import disflow
+            H, W = I0.shape[1:]
+            p = disflow.preset_params(disflow.Preset.MEDIUM, W, H)
+            res = multi.run_sharded(I0, I1, p, W, H, rank=rank, world=world, device=0, max_batch=4,
+                                    gather_flows=True)
+        else:
+            res = multi.run_sharded(I0, I1, None, 16, 12, rank=rank, world=world, compute=_fake_compute,
+                                    gather_flows=True)
+        if rank == 0:
+            out_q.put((res["digests"], res["flows"]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _gpu_pairs(n):
+    import disflow
+    pairs = [disflow.synth_pair(100 + k, 192, 144) for k in range(n)]
+    return np.stack([a for a, _ in pairs]), np.stack([b for _, b in pairs])
+
+
+def _run(world, n, use_gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, use_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    digests, flows = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    return digests, flows
+
+
+def test_gloo_world2_gathers_all_pairs_in_order():
+    n = 7
+    digests, flows = _run(2, n, use_gpu=False)
+    I0, I1 = _pairs(n)
+    single = multi.run_sharded(I0, I1, None, 16, 12, compute=_fake_compute, gather_flows=True)
+    assert digests == single["digests"]
+    assert np.array_equal(flows, single["flows"])
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_match_single_process():
+    import disflow
+    n = 6
+    digests, flows = _run(2, n, use_gpu=True)
+    I0, I1 = _gpu_pairs(n)
+    H, W = I0.shape[1:]
+    p = disflow.preset_params(disflow.Preset.MEDIUM, W, H)
+    single = multi.run_sharded(I0, I1, p, W, H, max_batch=6, gather_flows=True)
+    assert digests == single["digests"]
+    assert np.array_equal(flows.view(np.uint32), single["flows"].view(np.uint32))
