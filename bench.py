@@ -33,8 +33,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="pairs per GPU per step")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per step (0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch events")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per search launch (from tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -111,8 +112,9 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    eng.set_kernel_timing(True)
-    eng.kernel_time(disflow.KERNEL_SEARCH)  # reset accumulated records
+    if not a.no_kernel_timing:
+        eng.set_kernel_timing(True)
+        eng.kernel_time(disflow.KERNEL_SEARCH)  # reset accumulated records
 
     barrier()
     torch.cuda.synchronize(dev)

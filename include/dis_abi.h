@@ -153,8 +153,8 @@ dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* d
 
 /* Per-kernel timing with HIP events recorded on the context's launch stream
  * around every launch of the named kernel class (bench / roofline use).
- * kernel: 0 = pyramid, 1 = patch search (all levels), 2 = patch search
- * (finest level only), 3 = densify + upsample. */
+ * kernel: 0 = fused pyramid, 1 = patch search (all levels), 2 = patch search
+ * (finest level only), 3 = fused densify+upsample+crop. */
 dis_status dis_set_kernel_timing(dis_ctx* ctx, int enable);
 dis_status dis_kernel_time(dis_ctx* ctx, int kernel, int* launches, double* total_ms);
 

@@ -36,8 +36,17 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     __shared__ float buf1[(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
 
     const int tid = threadIdx.x;
-    const int tx = blockIdx.x * T0, ty = blockIdx.y * T0;
-    const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
+    // XCD-aware tile order: the dispatcher deals linear block ids round-robin
+    // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
+    // and horizontally adjacent tiles share their 128-B rows in one L2.
+    const int nbx = gridDim.x, nby = gridDim.y;
+    const int nb = nbx * nby * gridDim.z;
+    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    const int per = nb / 8;
+    const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
+    const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
+    const int tx = bx * T0, ty = by * T0;
+    const int pair = bz >> 1, frame = bz & 1;
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
     float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
 
@@ -138,18 +147,18 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     }
 }
 
-hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s)
+hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t)
 {
     const int T0 = 1 << a.levels;
     if (a.levels < 1 || a.levels > 6 || a.Wp % T0 || a.Hp % T0) return hipErrorInvalidValue;
     dim3 grid(a.Wp / T0, a.Hp / T0, 2 * batch);
     switch (a.levels) {
-        case 1: hipLaunchKernelGGL(k_pyramid<1>, grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_pyramid<2>, grid, dim3(256), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_pyramid<3>, grid, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_pyramid<4>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(k_pyramid<5>, grid, dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_pyramid<6>, grid, dim3(256), 0, s, a); break;
+        case 1: DIS_LAUNCH(t, k_pyramid<1>, grid, dim3(256), 0, s, a); break;
+        case 2: DIS_LAUNCH(t, k_pyramid<2>, grid, dim3(256), 0, s, a); break;
+        case 3: DIS_LAUNCH(t, k_pyramid<3>, grid, dim3(256), 0, s, a); break;
+        case 4: DIS_LAUNCH(t, k_pyramid<4>, grid, dim3(256), 0, s, a); break;
+        case 5: DIS_LAUNCH(t, k_pyramid<5>, grid, dim3(256), 0, s, a); break;
+        default: DIS_LAUNCH(t, k_pyramid<6>, grid, dim3(256), 0, s, a); break;
     }
     return hipGetLastError();
 }
@@ -329,14 +338,14 @@ bool output_fits(const OutputArgs& a)
     return pw <= kOutPX && ph <= kOutPY;
 }
 
-hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s)
+hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t)
 {
     if (!output_fits(a)) return hipErrorInvalidValue;
     dim3 grid((a.W + kOutTW - 1) / kOutTW, (a.H + kOutTH - 1) / kOutTH, batch);
     if (a.F == 0)
-        hipLaunchKernelGGL(k_output<false>, grid, dim3(256), 0, s, a);
+        DIS_LAUNCH(t, k_output<false>, grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(k_output<true>, grid, dim3(256), 0, s, a);
+        DIS_LAUNCH(t, k_output<true>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -1,9 +1,26 @@
 // dis_kernels.h -- kernel argument blocks and host launchers.
 #pragma once
 
+#include <hip/hip_ext.h>
+
 #include "dis_common.h"
 
 namespace dis {
+
+// Optional per-launch timing: events attached to the dispatch packet itself
+// (hipExtLaunchKernelGGL), so timing adds no extra queue packets.
+struct Timing {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+
+#define DIS_LAUNCH(T, kernel, grid, block, shmem, stream, ...)                                               \
+    do {                                                                                                    \
+        if ((T).start)                                                                                      \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, (T).start, (T).stop, 0, __VA_ARGS__); \
+        else                                                                                                \
+            hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                            \
+    } while (0)
 
 // One patch-search launch: one level, a batch of pairs.
 struct SearchArgs {
@@ -83,17 +100,17 @@ struct OutputArgs {
     float sc;
 };
 
-hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s);
+hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t = {});
 bool output_fits(const OutputArgs& a);
-hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s);
+hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_level0(const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,
                          const Geometry& g, float* img0, float* img1, int batch, hipStream_t s);
 hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int batch, hipStream_t s);
 hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, float* dy, int batch,
                         hipStream_t s);
-hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s);
+hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s, Timing t = {});
 int search8_tile_stride(int steps);
-hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s);
+hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 

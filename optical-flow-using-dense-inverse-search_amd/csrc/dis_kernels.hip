@@ -410,12 +410,12 @@ hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, 
     return hipGetLastError();
 }
 
-hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s)
+hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s, Timing t)
 {
     dim3 grid((a.n + 63) / 64, 1, batch);
     switch (ps) {
 #define DIS_CASE(P) \
-    case P: hipLaunchKernelGGL(k_search_generic<P>, grid, dim3(64), 0, s, a); break;
+    case P: DIS_LAUNCH(t, k_search_generic<P>, grid, dim3(64), 0, s, a); break;
         DIS_CASE(2)
         DIS_CASE(4)
         DIS_CASE(6)

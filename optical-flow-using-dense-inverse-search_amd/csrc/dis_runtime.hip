@@ -171,25 +171,19 @@ void free_ws(dis_ctx* c)
     c->in0 = c->in1 = nullptr;
 }
 
-// Kernel-timing bracket: records an event pair around one launch when enabled.
-struct TimeScope {
-    dis_ctx* c;
-    int kind;
-    hipStream_t s;
-    hipEvent_t b = nullptr;
-    TimeScope(dis_ctx* c_, int kind_, hipStream_t s_) : c(c_), kind(kind_), s(s_)
-    {
-        if (!c->timing || c->pool_next + 2 > c->pool.size()) return;
-        hipEvent_t a = c->pool[c->pool_next++];
-        b = c->pool[c->pool_next++];
-        hipEventRecord(a, s);
-        c->recs.push_back({kind, a, b});
-    }
-    ~TimeScope()
-    {
-        if (b) hipEventRecord(b, s);
-    }
-};
+// Per-launch timing: when enabled, hands out an event pair from the pool to be
+// attached to the next dispatch (hipExtLaunchKernelGGL) and books it under
+// `kind` (and `kind2` if >= 0).
+dis::Timing timing(dis_ctx* c, int kind, int kind2 = -1)
+{
+    dis::Timing t;
+    if (!c->timing || c->pool_next + 2 > c->pool.size()) return t;
+    t.start = c->pool[c->pool_next++];
+    t.stop = c->pool[c->pool_next++];
+    c->recs.push_back({kind, t.start, t.stop});
+    if (kind2 >= 0) c->recs.push_back({kind2, t.start, t.stop});
+    return t;
+}
 
 // Largest float s with sqrtf(s) <= thr (sqrtf is correctly rounded and
 // monotone, so `sqrtf(s) > thr` <=> `s > thr_sq`; src/patch.cpp:185).
@@ -230,7 +224,6 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
     float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant == 0;
     {
-        TimeScope t(c, 0, s);
         if (fast && g.C >= 1) {
             dis::PyramidArgs pa{};
             pa.I0 = I0;
@@ -252,7 +245,7 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
                 pa.off[l] = g.lv[l].plane_off;
                 pa.w[l] = g.lv[l].W;
             }
-            DIS_HIP(dis::launch_pyramid(pa, n, s));
+            DIS_HIP(dis::launch_pyramid(pa, n, s, timing(c, 0)));
             for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         } else {
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
@@ -318,13 +311,9 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
             b.tile_stride = dis::search8_tile_stride(L.steps);
             b.iters = g.iters;
             b.norm = g.norm;
-            TimeScope t1(c, 1, s);
-            TimeScope t2(c, l == g.F ? 2 : -1, s);
-            DIS_HIP(dis::launch_search8(b, n, s));
+            DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
-            TimeScope t1(c, 1, s);
-            TimeScope t2(c, l == g.F ? 2 : -1, s);
-            DIS_HIP(dis::launch_search_generic(a, g.ps, n, s));
+            DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         }
         if (fast && !c->debug) continue;  // the fused output kernel densifies the finest level itself
         dis::DensifyArgs d{};
@@ -340,7 +329,6 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
         d.nph = L.nph;
         d.offw = L.offw;
         d.offh = L.offh;
-        TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_densify(d, n, s));
     }
     dis::OutputArgs o{};
@@ -369,8 +357,7 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
         fused_out = dis::output_fits(o);
     }
     if (fused_out) {
-        TimeScope t(c, 3, s);
-        DIS_HIP(dis::launch_output(o, n, s));
+        DIS_HIP(dis::launch_output(o, n, s, timing(c, 3)));
     } else {
         if (fast && !c->debug) {  // the search loop skipped the finest densify: do it here
             const dis::LevelGeom& L = g.lv[g.F];
@@ -387,7 +374,6 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
             d.nph = L.nph;
             d.offw = L.offw;
             d.offh = L.offh;
-            TimeScope t(c, 3, s);
             DIS_HIP(dis::launch_densify(d, n, s));
         }
         const dis::LevelGeom& LF = g.lv[g.F];
@@ -405,7 +391,6 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
         u.sc = std::pow(2.0f, (float)g.F);
         u.inv_sc = 1.0 / (double)u.sc;
         u.xmax = upsample_xmax(g);
-        TimeScope t(c, 3, s);
         DIS_HIP(dis::launch_upsample(u, n, s));
     }
     return DIS_OK;

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of library builds in ONE process (cdna guide §5.4
+rule 24): each variant = path to a libdis_hip*.so [+ ":streams=N"]; rounds
+alternate variants; prints median/min ms per step and pairs/s per variant."""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "optical-flow-using-dense-inverse-search_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import disflow  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--preset", default="medium")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    a = ap.parse_args()
+    W, H, B = a.width, a.height, a.batch
+    dev = torch.device("cuda", 0)
+    pairs = [disflow.synth_pair(k, W, H) for k in range(B)]
+    d0 = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
+    d1 = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
+    outs, engines = [], []
+    for v in a.variants:
+        path, _, opt = v.partition(":")
+        disflow._lib = None
+        disflow.LIB_PATH = os.path.join(ROOT, path) if not os.path.isabs(path) else path
+        L = disflow.lib()
+        p = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
+        eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
+        if opt.startswith("streams="):
+            eng.set_concurrency(int(opt.split("=")[1]))
+        engines.append((v, L, eng))
+        outs.append(torch.empty((B, H, W, 2), dtype=torch.float32, device=dev))
+    s = torch.cuda.current_stream(dev)
+    times = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for (v, L, eng), out in zip(engines, outs):
+            disflow._lib = L
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            if r:  # round 0 is warm-up
+                times[v].append((time.perf_counter() - t0) / a.steps * 1e3)
+    ref = outs[0].cpu().numpy().view(np.uint32)
+    for (v, _, _), out in zip(engines, outs):
+        same = np.array_equal(out.cpu().numpy().view(np.uint32), ref)
+        t = times[v]
+        print(f"{v:70s} median {statistics.median(t):.3f} ms  min {min(t):.3f} ms  "
+              f"pairs/s {B / statistics.median(t) * 1e3:.0f}  same_as_first={same}")
+
+
+if __name__ == "__main__":
+    main()
