@@ -144,8 +144,9 @@ dis_status dis_set_debug(dis_ctx* ctx, int enable);
  * back into the caller's stream. Results do not depend on this setting. */
 dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
 
-/* Kernel variant: 0 = auto (specialised kernels where available, e.g. the
- * patch_size-8 search), 1 = generic kernels only. Both are bit-identical;
+/* Kernel variant: 0 = auto (specialised kernels where available: the
+ * patch_size-8 search with 2 lanes per patch), 1 = generic kernels only,
+ * 2 = the patch_size-8 search with 4 lanes per patch. All are bit-identical;
  * the switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);

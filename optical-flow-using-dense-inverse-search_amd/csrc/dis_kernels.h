@@ -56,6 +56,7 @@ struct Search8Args {
     float thr_sq;             // largest float s with sqrtf(s) <= outlierthresh
     int iters, norm;
     int tile_stride;          // LDS tile row stride (search8_tile_stride(steps))
+    int lanes_per_patch;      // 4 or 2 (k_search8<LPP>)
 };
 
 struct DensifyArgs {

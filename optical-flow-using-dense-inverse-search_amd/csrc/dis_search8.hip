@@ -8,12 +8,17 @@
 //   Patch::inverse_search                   src/patch.cpp:119-203,
 //   Patch::get_patch_second_image           src/patch.cpp:207-267.
 //
-// Mapping (CDNA4, wave64): 4 lanes per patch, 16 patches per wave; lane q of a
-// patch owns pixel columns q and q+4 (8 rows each). Eigen's SSE reduction of a
-// 64-vector (two 4-wide packet accumulators) is then exact:
-//   A_c  = sequential sum down column c          (in-lane, 7 adds)
-//   C_q  = A_q + A_{q+4}                          (in-lane)
-//   sum  = (C_0 + C_2) + (C_1 + C_3)              (two DPP quad_perm adds)
+// Mapping (CDNA4, wave64), template LPP = lanes per patch:
+//  LPP 4: 16 patches per wave; lane q owns pixel columns q and q+4. Eigen's SSE
+//         reduction of a 64-vector (two 4-wide packet accumulators; SURVEY.md
+//         A6) is then exact:  A_c = sequential sum down column c (in-lane),
+//         C_q = A_q + A_{q+4} (in-lane), sum = (C_0+C_2)+(C_1+C_3) (two DPP
+//         quad_perm adds, which also broadcast the sum to the 4 lanes).
+//  LPP 2: 32 patches per wave; lane q owns columns 4q..4q+3: A_c in-lane,
+//         C_j = A_j + A_{j+4} by one DPP add per j (commutative, so both lanes
+//         get C_0..C_3), then (C_0+C_2)+(C_1+C_3) in-lane. Fewer VALU
+//         instructions per sample (per-patch work is shared by 2 lanes, not 4)
+//         and fewer LDS taps (5 shared tap columns per lane), more registers.
 // A workgroup (4 waves) owns an 8x8 block of the patch grid and stages the
 // target image region every one of its patches can sample (start +-4 px,
 // SURVEY.md 7.3 "I1 search window") into one shared LDS tile. When the block's
@@ -44,28 +49,70 @@ __device__ __forceinline__ float quad_perm(float v)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
-// Eigen-order sum of the patch's 64 values held as x[0..7] (column q, rows
-// 0..7) and x[8..15] (column q+4) in each of the patch's 4 lanes.
-__device__ __forceinline__ float patch_sum(const float (&x)[16])
+template <int LPP>
+constexpr int kNCol = 8 / LPP;  // pixel columns per lane
+
+// pixel column (0..7) of lane q's ci-th column
+template <int LPP>
+__device__ __forceinline__ int lane_col(int q, int ci)
 {
-    float a = x[0];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) a = a + x[j];
-    float b = x[8];
-#pragma unroll
-    for (int j = 9; j < 16; ++j) b = b + x[j];
-    const float c = a + b;                        // C_q = A_q + A_{q+4}
-    const float t = c + quad_perm<kQuadXor2>(c);  // C_q + C_{q^2}
-    return t + quad_perm<kQuadXor1>(t);           // (C0+C2) + (C1+C3)
+    return LPP == 4 ? q + 4 * ci : 4 * q + ci;
 }
 
-template <typename Fn>
-__device__ __forceinline__ float patch_dot(const float (&g)[16], Fn&& r)
+// Eigen-order sum of the patch's 64 values; x[ci*8 + row] holds pixel (row,
+// lane_col(q, ci)) in lane q of the patch.
+template <int LPP>
+__device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 {
-    float x[16];
+    if constexpr (LPP == 4) {
+        float a = x[0];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = g[j] * r(j);
-    return patch_sum(x);
+        for (int j = 1; j < 8; ++j) a = a + x[j];
+        float b = x[8];
+#pragma unroll
+        for (int j = 9; j < 16; ++j) b = b + x[j];
+        const float c = a + b;                        // C_q = A_q + A_{q+4}
+        const float t = c + quad_perm<kQuadXor2>(c);  // C_q + C_{q^2}
+        return t + quad_perm<kQuadXor1>(t);           // (C0+C2) + (C1+C3)
+    } else {
+        float C[4];
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            float a = x[8 * ci];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) a = a + x[8 * ci + j];
+            C[ci] = a + quad_perm<kQuadXor1>(a);      // A_ci + A_{ci+4}
+        }
+        return (C[0] + C[2]) + (C[1] + C[3]);
+    }
+}
+
+// Eigen order of sum(g .* r): each product rounded, then accumulated in the
+// patch_sum order; products are formed inside the chains (no 32-value temp).
+template <int LPP, typename Fn>
+__device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&& r)
+{
+    if constexpr (LPP == 4) {
+        float a = g[0] * r(0);
+#pragma unroll
+        for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
+        float b = g[8] * r(8);
+#pragma unroll
+        for (int j = 9; j < 16; ++j) b = b + g[j] * r(j);
+        const float c = a + b;
+        const float t = c + quad_perm<kQuadXor2>(c);
+        return t + quad_perm<kQuadXor1>(t);
+    } else {
+        float C[4];
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            float a = g[8 * ci] * r(8 * ci);
+#pragma unroll
+            for (int j = 1; j < 8; ++j) a = a + g[8 * ci + j] * r(8 * ci + j);
+            C[ci] = a + quad_perm<kQuadXor1>(a);
+        }
+        return (C[0] + C[2]) + (C[1] + C[3]);
+    }
 }
 
 // Wave-wide min/max of an int (all 64 lanes participate).
@@ -104,48 +151,72 @@ __device__ __forceinline__ Warp warp_coefs(float x, float y)
     return w;
 }
 
-template <typename Tap>
-__device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[16])
+// `tap(k, c)` returns the target image at row Y-5+k (k = 0..8) and column
+// X-5 + (LPP == 4 ? q : 4q) + c.
+template <int LPP, typename Tap>
+__device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[8 * kNCol<LPP>])
 {
+    if constexpr (LPP == 4) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        float vb[9], va[9];
+        for (int s = 0; s < 2; ++s) {
+            float vb[9], va[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            vb[k] = tap(k, 4 * s);      // column X-5+c  (B / D taps)
-            va[k] = tap(k, 4 * s + 1);  // column X-4+c  (A / C taps)
+            for (int k = 0; k < 9; ++k) {
+                vb[k] = tap(k, 4 * s);      // column X-5+c  (B / D taps)
+                va[k] = tap(k, 4 * s + 1);  // column X-4+c  (A / C taps)
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // row Y-4+j: A = va[j+1], B = vb[j+1]; row Y-5+j: C = va[j], D = vb[j]
+                float t = w.w3 * va[j + 1];
+                t = t + w.w2 * vb[j + 1];
+                t = t + w.w1 * va[j];
+                t = t + w.w0 * vb[j];
+                r[8 * s + j] = t;
+            }
         }
+    } else {
+        // 5 shared tap columns, streamed row by row
+        float prev[5], cur[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) prev[c] = tap(0, c);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            // row Y-4+j: A = va[j+1], B = vb[j+1]; row Y-5+j: C = va[j], D = vb[j]
-            float t = w.w3 * va[j + 1];
-            t = t + w.w2 * vb[j + 1];
-            t = t + w.w1 * va[j];
-            t = t + w.w0 * vb[j];
-            r[8 * s + j] = t;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) cur[c] = tap(j + 1, c);
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) {
+                float t = w.w3 * cur[ci + 1];
+                t = t + w.w2 * cur[ci];
+                t = t + w.w1 * prev[ci + 1];
+                t = t + w.w0 * prev[ci];
+                r[8 * ci + j] = t;
+            }
+#pragma unroll
+            for (int c = 0; c < 5; ++c) prev[c] = cur[c];
         }
     }
     if (norm) {
-        const float mean = patch_sum(r) / 64.0f;  // sum / num_points_patch (:265)
+        const float mean = patch_sum<LPP>(r) / 64.0f;  // sum / num_points_patch (:265)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) r[j] = r[j] - mean;
+        for (int j = 0; j < 8 * kNCol<LPP>; ++j) r[j] = r[j] - mean;
     }
 }
 
 // The per-patch iteration (src/patch.cpp:156-203) with a given tap source.
-template <typename TapAt>
-__device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[16],
-                                        const float (&gy)[16], float rx, float ry, float ix, float iy,
+template <int LPP, typename TapAt>
+__device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[8 * kNCol<LPP>],
+                                        const float (&gy)[8 * kNCol<LPP>], float rx, float ry, float ix, float iy,
                                         float* pu0, float* pu1, TapAt&& tap_at)
 {
     float u0 = ix, u1 = iy;
     const float sx = rx + u0, sy = ry + u1;
-    float r[16];
+    float r[8 * kNCol<LPP>];
     Warp w = warp_coefs(sx, sy);
-    warp_patch(w, a.norm, tap_at(w), r);
+    warp_patch<LPP>(w, a.norm, tap_at(w), r);
     for (int counter = 1;; ++counter) {
-        const float b0 = patch_dot(gx, [&](int j) { return r[j]; });
-        const float b1 = patch_dot(gy, [&](int j) { return r[j]; });
+        const float b0 = patch_dot<LPP>(gx, [&](int j) { return r[j]; });
+        const float b1 = patch_dot<LPP>(gy, [&](int j) { return r[j]; });
         float d0, d1;
         lu2_solve(lu, b0, b1, &d0, &d1);
         u0 = u0 - d0;
@@ -163,7 +234,7 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
         }
         if (counter > a.iters) break;
         w = warp_coefs(px, py);
-        warp_patch(w, a.norm, tap_at(w), r);
+        warp_patch<LPP>(w, a.norm, tap_at(w), r);
     }
     *pu0 = u0;
     *pu1 = u1;
@@ -171,9 +242,15 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 
 }  // namespace
 
-// grid: (ceil(npw/8), ceil(nph/8), batch); block 256
-__global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args a)
+template <int LPP>
+constexpr int kWaves = LPP == 4 ? DIS_SEARCH8_WAVES : 4;  // min waves per SIMD (VGPR cap 512/k)
+
+// grid: (ceil(npw/8), ceil(nph/8), batch); block 64*LPP threads = 8x8 patches
+template <int LPP>
+__global__ void __launch_bounds__(64 * LPP) __attribute__((amdgpu_waves_per_eu(kWaves<LPP>)))
+k_search8(Search8Args a)
 {
+    constexpr int NT = 64 * LPP, NW = LPP, NC = kNCol<LPP>;
     __shared__ float tile[kTileMax * kTSMax];
     __shared__ float2 cu[192];   // staged coarse patch displacements (<= 12 x 12)
     __shared__ int2 crng[2 * 8];  // per block column/row: covering coarse range
@@ -181,9 +258,9 @@ __global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args 
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int q = lane & 3, pw = lane >> 2;  // lane in patch, patch in wave
-    const int gx = blockIdx.x * kBG + wave * 2 + (pw >> 3);
-    const int gy = blockIdx.y * kBG + (pw & 7);
+    const int q = tid % LPP, pb = tid / LPP;  // lane in patch, patch in block
+    const int gx = blockIdx.x * kBG + (pb >> 3);
+    const int gy = blockIdx.y * kBG + (pb & 7);
     const int pair = blockIdx.z;
     const bool active = gx < a.npw && gy < a.nph;
     const int W = a.W, H = a.H;
@@ -202,51 +279,59 @@ __global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args 
 
     // --- template gradients: Sobel (ksize 3, 1/8, reflect-101) of the level
     // image at pixels (rx-4+c, ry-4+j), zero outside the image (zero-padded
-    // dx/dy planes, src/main.cpp:45-47). Lane q: columns q and q+4.
-    float gdx[16], gdy[16];
+    // dx/dy planes, src/main.cpp:45-47). Lane q: columns lane_col(q, ci).
+    float gdx[8 * NC], gdy[8 * NC];
     if (active) {
+        // NC == 2 owns columns q, q+4 (3 loads each); NC == 4 owns 4 adjacent
+        // columns sharing a 6-column window. All 60 loads are issued before
+        // use (a row-streamed variant that holds fewer registers measured 3%
+        // slower: less memory-level parallelism in the prologue).
+        constexpr int NX = (NC == 2) ? 6 : 6;
+        int xs[NX];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int px = irx - 4 + q + 4 * s;
-            const bool colin = px >= 0 && px < W;
-            const int xm = clampi(reflect101(px - 1, W), 0, W - 1);
-            const int xc = clampi(px, 0, W - 1);
-            const int xp = clampi(reflect101(px + 1, W), 0, W - 1);
-            float R[10], S[10];
+        for (int m = 0; m < NX; ++m) {
+            const int col = (NC == 2) ? (irx - 4 + q + 4 * (m / 3) + (m % 3) - 1) : (irx - 5 + 4 * q + m);
+            xs[m] = clampi(reflect101(col, W), 0, W - 1);
+        }
+        float R[NC][10], S[NC][10];
 #pragma unroll
-            for (int k = 0; k < 10; ++k) {
-                const int yy = clampi(reflect101(iry - 5 + k, H), 0, H - 1);
-                const float* row = I0 + (size_t)yy * W;
-                const float l = row[xm], c = row[xc], rr = row[xp];
-                R[k] = rr - l;
-                S[k] = c * 0.25f + (l + rr) * 0.125f;
+        for (int k = 0; k < 10; ++k) {
+            const int yy = clampi(reflect101(iry - 5 + k, H), 0, H - 1);
+            const float* row = I0 + (size_t)yy * W;
+            float v[NX];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) v[m] = row[xs[m]];
+#pragma unroll
+            for (int ci = 0; ci < NC; ++ci) {
+                const int m0 = (NC == 2) ? 3 * ci : ci;
+                const float l = v[m0], c = v[m0 + 1], rr = v[m0 + 2];
+                R[ci][k] = rr - l;
+                S[ci][k] = c * 0.25f + (l + rr) * 0.125f;
             }
+        }
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) {
+            const int px = irx - 4 + lane_col<LPP>(q, ci);
+            const bool colin = px >= 0 && px < W;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int py = iry - 4 + j;
                 const bool in = colin && py >= 0 && py < H;
-                const float dx = R[j + 1] * 0.25f + (R[j] + R[j + 2]) * 0.125f;
-                const float dy = S[j + 2] - S[j];
-                gdx[8 * s + j] = in ? dx : 0.0f;
-                gdy[8 * s + j] = in ? dy : 0.0f;
+                const float dx = R[ci][j + 1] * 0.25f + (R[ci][j] + R[ci][j + 2]) * 0.125f;
+                const float dy = S[ci][j + 2] - S[ci][j];
+                gdx[8 * ci + j] = in ? dx : 0.0f;
+                gdy[8 * ci + j] = in ? dy : 0.0f;
             }
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) gdx[j] = gdy[j] = 0.0f;
+        for (int j = 0; j < 8 * NC; ++j) gdx[j] = gdy[j] = 0.0f;
     }
     LU2 lu;
     {
-        float x[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) x[j] = gdx[j] * gdx[j];
-        const float h00 = patch_sum(x);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) x[j] = gdx[j] * gdy[j];
-        const float h01 = patch_sum(x);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) x[j] = gdy[j] * gdy[j];
-        const float h11 = patch_sum(x);
+        const float h00 = patch_dot<LPP>(gdx, [&](int j) { return gdx[j]; });
+        const float h01 = patch_dot<LPP>(gdx, [&](int j) { return gdy[j]; });
+        const float h11 = patch_dot<LPP>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
 
@@ -268,13 +353,14 @@ __global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args 
         const int hb = min(a.c_nph - 1, floordiv(yhi - a.c_offh + hp, st));
         const int PH = hb - ha + 1, PN = (gb - ga + 1) * PH;  // <= 12 x 12 (host-checked)
         const float2* uc = a.u_coarse + (size_t)pair * a.u_stride;
-        if (tid < PN) {
-            const int cx = tid / PH, cy = tid - cx * PH;
-            cu[tid] = uc[(ga + cx) * a.c_nph + ha + cy];
-        } else if (tid >= 192 && tid < 192 + 2 * kBG) {
+        for (int i = tid; i < PN; i += NT) {
+            const int cx = i / PH, cy = i - cx * PH;
+            cu[i] = uc[(ga + cx) * a.c_nph + ha + cy];
+        }
+        if (tid < 2 * kBG) {
             // covering coarse-patch range per block column / row (src/patch_grid.cpp:121-182
             // footprint test), relative to the staged block
-            const int t = tid - 192;
+            const int t = tid;
             if (t < kBG) {
                 const int x = ((bgx0 + t) * st + a.offw) >> 1;  // floor(ref.x / 2)
                 crng[t] = make_int2(max(floordiv(x - a.c_offw - hp + st, st), ga) - ga,
@@ -337,28 +423,30 @@ __global__ void __launch_bounds__(256, DIS_SEARCH8_WAVES) k_search8(Search8Args 
     float u0 = ix, u1 = iy;
     if (use_tile) {
         // all of this wave's rows in flight at once, then the LDS stores
-        float v[kTileMax / 4];
+        float v[kTileMax / NW];
         const int cx = clampi(tx0 + lane, 0, W - 1);
 #pragma unroll
-        for (int j = 0; j < kTileMax / 4; ++j) {
-            const int r = wave + 4 * j;
+        for (int j = 0; j < kTileMax / NW; ++j) {
+            const int r = wave + NW * j;
             v[j] = (r < th && lane < tw) ? I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + cx] : 0.0f;
         }
 #pragma unroll
-        for (int j = 0; j < kTileMax / 4; ++j) {
-            const int r = wave + 4 * j;
+        for (int j = 0; j < kTileMax / NW; ++j) {
+            const int r = wave + NW * j;
             if (r < th && lane < tw) tile[r * TS + lane] = v[j];
         }
         __syncthreads();
         if (valid) {
-            iterate(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
-                const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + q - tx0);
+            const int qb = LPP == 4 ? q : 4 * q;  // lane's first tap column
+            iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+                const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
                 return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
         }
     } else if (valid) {
-        iterate(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
-            const int y0 = w.Y - 5, x0 = w.X - 5 + q;
+        const int qb = LPP == 4 ? q : 4 * q;
+        iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+            const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
             return [=](int k, int c) {
                 return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
             };
@@ -393,7 +481,10 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
 {
     if (a.tile_stride < kTileMax + 1 || a.tile_stride > kTSMax) return hipErrorInvalidValue;
     dim3 grid((a.npw + kBG - 1) / kBG, (a.nph + kBG - 1) / kBG, batch);
-    DIS_LAUNCH(t, k_search8, grid, dim3(256), 0, s, a);
+    if (a.lanes_per_patch == 2)
+        DIS_LAUNCH(t, k_search8<2>, grid, dim3(128), 0, s, a);
+    else
+        DIS_LAUNCH(t, k_search8<4>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -233,7 +233,7 @@ class DenseInverseSearch:
                                        MEM_DEVICE, stream or None))
 
     def set_variant(self, variant: int) -> None:
-        """0 = specialised kernels where available, 1 = generic kernels only."""
+        """0 = specialised kernels (2 lanes/patch search), 1 = generic only, 2 = 4 lanes/patch."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
 
     def set_concurrency(self, streams: int) -> None:

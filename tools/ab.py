@@ -40,8 +40,14 @@ def main():
         L = disflow.lib()
         p = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
         eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
-        if opt.startswith("streams="):
-            eng.set_concurrency(int(opt.split("=")[1]))
+        for kv in filter(None, opt.split(",")):
+            k, _, val = kv.partition("=")
+            if k == "streams":
+                eng.set_concurrency(int(val))
+            elif k == "variant":
+                eng.set_variant(int(val))
+            else:
+                raise SystemExit(f"unknown option {k}")
         engines.append((v, L, eng))
         outs.append(torch.empty((B, H, W, 2), dtype=torch.float32, device=dev))
     s = torch.cuda.current_stream(dev)
