@@ -149,7 +149,10 @@ def main():
                          f"C oracle (oracle/dis_oracle.c, gcc -O2 -ffp-contract=off), one host thread"}
 
     avg_ms = ms_s / max(n_s, 1)
-    bytes_per_launch = B * wl["search_bytes_all"] / wl["search_launches"]
+    # the batch runs as sub-batches on concurrent streams: bytes per launch =
+    # the step's search bytes / the step's search launches
+    launches_per_step = n_s / a.steps if n_s else wl["search_launches"]
+    bytes_per_launch = B * wl["search_bytes_all"] / launches_per_step
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if n_s else None
     traffic = None
     if os.path.exists(a.traffic_json):
@@ -184,6 +187,9 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "avg_launch_ms": avg_ms, "launches": n_s,
+                         "note": "per-launch HIP-event durations of k_search8 (one launch per level per "
+                                 "sub-batch stream; the 2 streams' launches overlap, so durations include "
+                                 "co-running time); kernel is VALU-bound, see DESIGN.md",
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
             "cpu_baseline": cpu,
