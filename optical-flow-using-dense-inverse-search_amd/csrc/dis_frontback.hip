@@ -26,14 +26,19 @@ namespace {
 // grid: (Wp / T0, Hp / T0, 2 * batch), block 256; z = pair*2 + frame.
 // LEVELS (1..6) is a template parameter so every load loop has a compile-time
 // trip count and all of a thread's loads are in flight at once.
+#ifndef DIS_PYR_THREADS
+#define DIS_PYR_THREADS 256
+#endif
+constexpr int kPyrT = DIS_PYR_THREADS;  // threads per pyramid workgroup
+
 template <int LEVELS>
-__global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
+__global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
 {
-    constexpr int T0 = 1 << LEVELS, SS = T0 + 2, NLOAD = (SS * SS + 255) / 256;
+    constexpr int T0 = 1 << LEVELS, SS = T0 + 2, NLOAD = (SS * SS + kPyrT - 1) / kPyrT;
     constexpr int N1 = T0 / 2;
-    __shared__ uint8_t src[SS * SS];
-    __shared__ float buf0[N1 * N1];
-    __shared__ float buf1[(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
+    __shared__ uint8_t srcs[2][SS * SS];
+    __shared__ float bufs0[2][N1 * N1];
+    __shared__ float bufs1[2][(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
 
     const int tid = threadIdx.x;
     // XCD-aware tile order: the dispatcher deals linear block ids round-robin
@@ -46,9 +51,7 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
     const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
     const int tx = bx * T0, ty = by * T0;
-    const int pair = bz >> 1, frame = bz & 1;
-    const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-    float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+    const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
 
     // u8 tile with a 1-pixel halo: replicate padding to Wp x Hp (floor/ceil
     // split) composed with Sobel's reflect-101 at the Wp x Hp border. Wave w
@@ -56,72 +59,95 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     // column index is computed once per lane.
     {
         const int lane = tid & 63, wave = tid >> 6;
-        constexpr int NR = (SS + 3) / 4;  // rows per wave
+        constexpr int NWV = kPyrT / 64, NR = (SS + NWV - 1) / NWV;  // rows per wave
         const int c0 = lane, c1 = lane + 64;
         const int xs0 = clampi(reflect101(tx - 1 + c0, a.Wp) - a.pl, 0, a.W - 1);
         const int xs1 = clampi(reflect101(tx - 1 + min(c1, SS - 1), a.Wp) - a.pl, 0, a.W - 1);
-        uint8_t v0[NR], v1[NR];
+        uint8_t v0[2][NR], v1[2][NR];
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const int r = wave + 4 * j;
-            const int ys = clampi(reflect101(ty - 1 + min(r, SS - 1), a.Hp) - a.pt, 0, a.H - 1);
-            const uint8_t* row = in + (size_t)__builtin_amdgcn_readfirstlane(ys) * a.stride;
-            v0[j] = (c0 < SS) ? row[xs0] : 0;
-            v1[j] = (c1 < SS) ? row[xs1] : 0;
-        }
+        for (int f = 0; f < 2; ++f) {
+            const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const int r = wave + 4 * j;
-            if (r < SS) {
-                if (c0 < SS) src[r * SS + c0] = v0[j];
-                if (c1 < SS) src[r * SS + c1] = v1[j];
+            for (int j = 0; j < NR; ++j) {
+                const int r = wave + NWV * j;
+                const int ys = clampi(reflect101(ty - 1 + min(r, SS - 1), a.Hp) - a.pt, 0, a.H - 1);
+                const uint8_t* row = in + (size_t)__builtin_amdgcn_readfirstlane(ys) * a.stride;
+                v0[f][j] = (c0 < SS) ? row[xs0] : 0;
+                v1[f][j] = (c1 < SS) ? row[xs1] : 0;
             }
         }
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const int r = wave + NWV * j;
+                if (r < SS) {
+                    if (c0 < SS) srcs[f][r * SS + c0] = v0[f][j];
+                    if (c1 < SS) srcs[f][r * SS + c1] = v1[f][j];
+                }
+            }
     }
     __syncthreads();
 
-    // level 1 (and level 0 when requested)
 #pragma unroll
-    for (int k0 = 0; k0 < N1 * N1; k0 += 256) {
+    for (int f = 0; f < 2; ++f) {
+    const uint8_t* src = srcs[f];
+    float* buf0 = bufs0[f];
+    float* buf1 = bufs1[f];
+    float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+    // level 1 (and level 0 when requested). A work item is a 2x2 block of
+    // level-1 pixels = a 4x4 block of level-0 magnitudes read from a 6x6 u8
+    // window; the separable Sobel row sums R/S are shared by the 16 pixels.
+    constexpr int B1 = N1 >= 2 ? 2 : 1;  // level-1 block edge
+    constexpr int NB = N1 / B1;          // blocks per tile edge
+    constexpr int E0 = 2 * B1;           // level-0 block edge
+#pragma unroll
+    for (int k0 = 0; k0 < NB * NB; k0 += kPyrT) {
         const int k = k0 + tid;
-        if (N1 * N1 % 256 != 0 && k >= N1 * N1) break;
-        const int y1 = k / N1, x1 = k - y1 * N1;
-        float v[4][4];
+        if (NB * NB % kPyrT != 0 && k >= NB * NB) break;
+        const int by = k / NB, bx = k - by * NB;
+        float R[E0 + 2][E0], S[E0 + 2][E0];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < E0 + 2; ++r) {
+            float v[E0 + 2];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) v[r][c] = (float)src[(2 * y1 + r) * SS + 2 * x1 + c];
-        float m[2][2];
+            for (int c = 0; c < E0 + 2; ++c) v[c] = (float)src[(E0 * by + r) * SS + E0 * bx + c];
 #pragma unroll
-        for (int dc = 0; dc < 2; ++dc) {
-            float R[4], S[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                R[r] = v[r][dc + 2] - v[r][dc];
-                S[r] = v[r][dc + 1] * 0.25f + (v[r][dc] + v[r][dc + 2]) * 0.125f;
+            for (int c = 0; c < E0; ++c) {
+                R[r][c] = v[c + 2] - v[c];
+                S[r][c] = v[c + 1] * 0.25f + (v[c] + v[c + 2]) * 0.125f;
             }
+        }
+        float m[E0][E0];
 #pragma unroll
-            for (int dr = 0; dr < 2; ++dr) {
-                const float gx = R[dr + 1] * 0.25f + (R[dr] + R[dr + 2]) * 0.125f;
-                const float gy = S[dr + 2] - S[dr];
+        for (int r = 0; r < E0; ++r)
+#pragma unroll
+            for (int c = 0; c < E0; ++c) {
+                const float gx = R[r + 1][c] * 0.25f + (R[r][c] + R[r + 2][c]) * 0.125f;
+                const float gy = S[r + 2][c] - S[r][c];
                 const float t1 = gx * gx, t2 = gy * gy;
                 const float s = t1 + t2;
-                m[dr][dc] = sqrtf(s);
+                m[r][c] = sqrtf(s);
             }
-        }
         if (a.write_l0) {
-            float* p0 = planes + (size_t)(ty + 2 * y1) * a.Wp + tx + 2 * x1;
-            p0[0] = m[0][0];
-            p0[1] = m[0][1];
-            p0[a.Wp] = m[1][0];
-            p0[a.Wp + 1] = m[1][1];
+#pragma unroll
+            for (int r = 0; r < E0; ++r)
+#pragma unroll
+                for (int c = 0; c < E0; ++c)
+                    planes[(size_t)(ty + E0 * by + r) * a.Wp + tx + E0 * bx + c] = m[r][c];
         }
-        float s = m[0][0] + m[0][1];
-        s = s + m[1][0];
-        s = s + m[1][1];
-        const float l1 = s * 0.25f;
-        buf0[k] = l1;
-        planes[a.off[1] + (size_t)(ty / 2 + y1) * a.w[1] + tx / 2 + x1] = l1;
+#pragma unroll
+        for (int i = 0; i < B1; ++i)
+#pragma unroll
+            for (int j = 0; j < B1; ++j) {
+                float s = m[2 * i][2 * j] + m[2 * i][2 * j + 1];
+                s = s + m[2 * i + 1][2 * j];
+                s = s + m[2 * i + 1][2 * j + 1];
+                const float l1 = s * 0.25f;
+                const int y1 = B1 * by + i, x1 = B1 * bx + j;
+                buf0[y1 * N1 + x1] = l1;
+                planes[a.off[1] + (size_t)(ty / 2 + y1) * a.w[1] + tx / 2 + x1] = l1;
+            }
     }
 
     // levels 2..LEVELS from LDS, ping-pong buf0 <-> buf1
@@ -131,7 +157,7 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
     for (int l = 2; l <= LEVELS; ++l) {
         __syncthreads();
         const int ns = T0 >> (l - 1), nd = ns / 2;
-        for (int k = tid; k < nd * nd; k += 256) {
+        for (int k = tid; k < nd * nd; k += kPyrT) {
             const int y = k / nd, x = k - y * nd;
             const float* p = cur + (2 * y) * ns + 2 * x;
             float s = p[0] + p[1];
@@ -145,20 +171,21 @@ __global__ void __launch_bounds__(256) k_pyramid(PyramidArgs a)
         cur = nxt;
         nxt = t;
     }
+    }
 }
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t)
 {
     const int T0 = 1 << a.levels;
     if (a.levels < 1 || a.levels > 6 || a.Wp % T0 || a.Hp % T0) return hipErrorInvalidValue;
-    dim3 grid(a.Wp / T0, a.Hp / T0, 2 * batch);
+    dim3 grid(a.Wp / T0, a.Hp / T0, batch);
     switch (a.levels) {
-        case 1: DIS_LAUNCH(t, k_pyramid<1>, grid, dim3(256), 0, s, a); break;
-        case 2: DIS_LAUNCH(t, k_pyramid<2>, grid, dim3(256), 0, s, a); break;
-        case 3: DIS_LAUNCH(t, k_pyramid<3>, grid, dim3(256), 0, s, a); break;
-        case 4: DIS_LAUNCH(t, k_pyramid<4>, grid, dim3(256), 0, s, a); break;
-        case 5: DIS_LAUNCH(t, k_pyramid<5>, grid, dim3(256), 0, s, a); break;
-        default: DIS_LAUNCH(t, k_pyramid<6>, grid, dim3(256), 0, s, a); break;
+        case 1: DIS_LAUNCH(t, k_pyramid<1>, grid, dim3(kPyrT), 0, s, a); break;
+        case 2: DIS_LAUNCH(t, k_pyramid<2>, grid, dim3(kPyrT), 0, s, a); break;
+        case 3: DIS_LAUNCH(t, k_pyramid<3>, grid, dim3(kPyrT), 0, s, a); break;
+        case 4: DIS_LAUNCH(t, k_pyramid<4>, grid, dim3(kPyrT), 0, s, a); break;
+        case 5: DIS_LAUNCH(t, k_pyramid<5>, grid, dim3(kPyrT), 0, s, a); break;
+        default: DIS_LAUNCH(t, k_pyramid<6>, grid, dim3(kPyrT), 0, s, a); break;
     }
     return hipGetLastError();
 }
@@ -168,10 +195,25 @@ hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr int kOutTW = 64, kOutTH = 16;  // full-resolution output tile per workgroup
-constexpr int kOutSW = kOutTW + 3;       // level-F dense window bound (F == 0 is the widest)
-constexpr int kOutSH = kOutTH + 3;
-constexpr int kOutPX = 48, kOutPY = 32;  // staged patch block (grid columns x rows)
+#ifndef DIS_OUT_TH
+#define DIS_OUT_TH 64  // measured: 64 rows beat 16 by 2.3% of the step (F >= 1)
+#endif
+constexpr int kOutTW = 64, kOutTH = DIS_OUT_TH;  // full-resolution output tile per workgroup
+
+// LDS shapes per instantiation: level-F window (F == 0 is the widest; F >= 1
+// needs half the tile + the interpolation halo) and the staged patch block for
+// K = ceil(ps/steps) covering patches per axis (steps >= ceil(8/K), ps = 8).
+template <bool UPS>
+struct OutShape {
+    static constexpr int SW = UPS ? kOutTW / 2 + 3 : kOutTW + 3;
+    static constexpr int SH = UPS ? kOutTH / 2 + 3 : kOutTH + 3;
+};
+template <bool UPS, int K>
+struct OutPatch {
+    static constexpr int st = (8 + K - 1) / K;
+    static constexpr int PX = (OutShape<UPS>::SW + 7) / st + 2;
+    static constexpr int PY = (OutShape<UPS>::SH + 7) / st + 2;
+};
 
 // cv::resize INTER_LINEAR source index / fraction for destination index d at
 // scale 2^F: s = (d + .5) * 2^-F - .5 (exact dyadic in float), clamped.
@@ -198,9 +240,13 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 // 1) stage the patch displacements covering this tile's level-F window in LDS
 //    (one round of loads), 2) densify the window into LDS (src/patch_grid.cpp:
 //    121-182), 3) F == 0: crop; F >= 1: scale by 2^F, resize, crop.
-template <bool UPSAMPLE>
+// K = ceil(ps / steps) bounds the covering patches per axis, so the gather is
+// an unrolled, predicated K x K loop (no divergent loops).
+template <bool UPSAMPLE, int K>
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
+    constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
+    constexpr int kOutPX = OutPatch<UPSAMPLE, K>::PX, kOutPY = OutPatch<UPSAMPLE, K>::PY;
     __shared__ float2 pu[kOutPX * kOutPY];
     __shared__ float2 dense[kOutSW * kOutSH];
     __shared__ int2 cr[kOutSW], rr[kOutSH];
@@ -232,7 +278,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const int ha = max(0, floordiv(j0 - a.offh - hp + st, st)), hb = min(a.nph - 1, floordiv(j1 - a.offh + hp, st));
     const int PW = gb - ga + 1, PH = hb - ha + 1;  // <= kOutPX x kOutPY (output_fits)
     {
-        constexpr int NL = kOutPX * kOutPY / 256;
+        constexpr int NL = (kOutPX * kOutPY + 255) / 256;
         float2 v[NL];
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
@@ -240,15 +286,18 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const int cx = k / kOutPY, cy = k % kOutPY;
             v[j] = (cx < PW && cy < PH) ? u[(ga + cx) * a.nph + ha + cy] : make_float2(0.f, 0.f);
         }
+        // new_u = u * 0.5 (src/patch_grid.cpp:156), formed once per patch
 #pragma unroll
-        for (int j = 0; j < NL; ++j) pu[tid + 256 * j] = v[j];
+        for (int j = 0; j < NL; ++j)
+            if (tid + 256 * j < kOutPX * kOutPY) pu[tid + 256 * j] = make_float2(v[j].x * 0.5f, v[j].y * 0.5f);
     }
     // covering patch ranges per window column / row (one floordiv pair each)
     if (tid < rw) {
         const int px = i0 + tid;
         cr[tid] = make_int2(max(floordiv(px - a.offw - hp + st, st), ga) - ga,
                             min(floordiv(px - a.offw + hp, st), gb) - ga);
-    } else if (tid >= 128 && tid - 128 < rh) {
+    }
+    if (tid >= 128 && tid - 128 < rh) {
         const int py = j0 + tid - 128;
         rr[tid - 128] = make_int2(max(floordiv(py - a.offh - hp + st, st), ha) - ha,
                                   min(floordiv(py - a.offh + hp, st), hb) - ha);
@@ -257,15 +306,19 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const float sc = a.sc;
     for (int k = tid; k < rw * rh; k += 256) {
         const int r = k / rw, c = k - r * rw;
-        // dense_at() over the staged displacements: patch-id order, f from +0
+        // dense value: contributions in patch-id order, f from +0; masked
+        // terms add +0, an exact no-op (f is never -0)
         const int2 xr = cr[c], yr = rr[r];
         float fx = 0.0f, fy = 0.0f, w = 0.0f;
-        for (int gx = xr.x; gx <= xr.y; ++gx)
-            for (int gy = yr.x; gy <= yr.y; ++gy) {
-                const float2 t = pu[gx * kOutPY + gy];
-                fx = fx + t.x * 0.5f;
-                fy = fy + t.y * 0.5f;
-                w = w + 0.5f;
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const bool ok = (xr.x + i <= xr.y) && (yr.x + j <= yr.y);
+                const float2 t = pu[ok ? (xr.x + i) * kOutPY + yr.x + j : 0];
+                fx = fx + (ok ? t.x : 0.0f);
+                fy = fy + (ok ? t.y : 0.0f);
+                w = w + (ok ? 0.5f : 0.0f);
             }
         if (w > 0) {
             fx = fx / w;
@@ -276,9 +329,10 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     }
     __syncthreads();
 
-    const int px = ox + (tid & 31) * 2, py = oy + (tid >> 5) * 2;
+    constexpr int RPT = kOutTH / 8;  // output rows per thread
+    const int px = ox + (tid & 31) * 2, py = oy + (tid >> 5) * RPT;
 #pragma unroll
-    for (int dy = 0; dy < 2; ++dy) {
+    for (int dy = 0; dy < RPT; ++dy) {
         const int y = py + dy;
         if (y >= a.H) continue;
         float2 o[2];
@@ -333,19 +387,31 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 
 bool output_fits(const OutputArgs& a)
 {
-    // the staged patch block must fit: (window + ps) / steps + 1 per axis
-    const int pw = (kOutSW + 2 * a.hp) / a.steps + 2, ph = (kOutSH + 2 * a.hp) / a.steps + 2;
-    return pw <= kOutPX && ph <= kOutPY;
+    // patch size 8 (the fast path), at most 4 covering patches per axis
+    // (steps >= 2); the LDS shapes above are derived from exactly that
+    return a.hp == 4 && a.steps >= 2;
+}
+
+template <int K>
+static void launch_output_k(const OutputArgs& a, dim3 grid, hipStream_t s, Timing t)
+{
+    if (a.F == 0)
+        DIS_LAUNCH(t, (k_output<false, K>), grid, dim3(256), 0, s, a);
+    else
+        DIS_LAUNCH(t, (k_output<true, K>), grid, dim3(256), 0, s, a);
 }
 
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t)
 {
     if (!output_fits(a)) return hipErrorInvalidValue;
     dim3 grid((a.W + kOutTW - 1) / kOutTW, (a.H + kOutTH - 1) / kOutTH, batch);
-    if (a.F == 0)
-        DIS_LAUNCH(t, k_output<false>, grid, dim3(256), 0, s, a);
-    else
-        DIS_LAUNCH(t, k_output<true>, grid, dim3(256), 0, s, a);
+    switch ((2 * a.hp + a.steps - 1) / a.steps) {  // K = ceil(ps / steps)
+        case 1: launch_output_k<1>(a, grid, s, t); break;
+        case 2: launch_output_k<2>(a, grid, s, t); break;
+        case 3: launch_output_k<3>(a, grid, s, t); break;
+        case 4: launch_output_k<4>(a, grid, s, t); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
