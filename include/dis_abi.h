@@ -145,9 +145,10 @@ dis_status dis_set_debug(dis_ctx* ctx, int enable);
 dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
 
 /* Kernel variant: 0 = auto (specialised kernels where available: the
- * patch_size-8 search with 2 lanes per patch), 1 = generic kernels only,
- * 2 = the patch_size-8 search with 4 lanes per patch. All are bit-identical;
- * the switch exists for parity tests and A/B timing. */
+ * patch_size-8 search with 8 lanes per patch on levels with few patches and 2
+ * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 = the
+ * patch_size-8 search with 4 / 2 / 8 lanes per patch on every level. All are
+ * bit-identical; the switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
 dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);

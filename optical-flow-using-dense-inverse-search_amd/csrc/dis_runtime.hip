@@ -92,13 +92,34 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
+#ifndef DIS_LPP8_MAX_PATCHES
+#define DIS_LPP8_MAX_PATCHES 65536  // level patches x pairs up to which 8 lanes/patch is used
+#endif
+#ifndef DIS_LPP4_MAX_PATCHES
+#define DIS_LPP4_MAX_PATCHES 0      // ... and 4 lanes/patch (above: 2 lanes/patch)
+#endif
+
+// Lanes per patch for the patch_size-8 search at one level. Few patches leave
+// the chip idle and the level is bound by one wave's serial iteration chain:
+// spend more lanes per patch (shorter chain). Many patches make it VALU-bound:
+// 2 lanes per patch does the least total work.
+static int search8_lanes(int variant, long long patches)
+{
+    if (variant == 2) return 4;
+    if (variant == 3) return 2;
+    if (variant == 4) return 8;
+    if (patches <= DIS_LPP8_MAX_PATCHES) return 8;
+    if (patches <= DIS_LPP4_MAX_PATCHES) return 4;
+    return 2;
+}
+
 struct dis_ctx {
     dis_params p;
     dis::Geometry g;
     int device = 0;
     int max_batch = 1;
     int debug = 0;
-    int variant = 0;  // 0 auto (fast kernels, 2 lanes/patch), 1 generic only, 2 fast with 4 lanes/patch
+    int variant = 0;  // 0 auto, 1 generic only, 2/3/4: patch_size-8 search with 4/2/8 lanes per patch
     int last_batch = 0;
     hipStream_t own = nullptr;
     static constexpr int kMaxSub = 8;
@@ -309,7 +330,7 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
             b.tmp_ub_h = L.tmp_ub_h;
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
             b.tile_stride = dis::search8_tile_stride(L.steps);
-            b.lanes_per_patch = c->variant == 2 ? 4 : 2;  // 2 lanes/patch measured 5% faster
+            b.lanes_per_patch = search8_lanes(c->variant, (long long)L.npw * L.nph * n);
             b.iters = g.iters;
             b.norm = g.norm;
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
@@ -634,7 +655,7 @@ dis_status dis_set_concurrency(dis_ctx* c, int streams)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 2) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0, 1 or 2");
+    if (variant < 0 || variant > 4) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..4");
     c->variant = variant;
     return DIS_OK;
 }

@@ -19,7 +19,12 @@
 //         get C_0..C_3), then (C_0+C_2)+(C_1+C_3) in-lane. Fewer VALU
 //         instructions per sample (per-patch work is shared by 2 lanes, not 4)
 //         and fewer LDS taps (5 shared tap columns per lane), more registers.
-// A workgroup (4 waves) owns an 8x8 block of the patch grid and stages the
+//  LPP 8: 8 patches per wave, one pixel column per lane (lowest latency per
+//         patch; chosen for coarse levels, whose few patches leave the chip
+//         idle). A patch's lanes are {4h..4h+3} and {4h+8..4h+11} of a 16-lane
+//         row (h = 0, 1), holding columns 0..3 and 4..7, so C_q = A_q + A_{q+4}
+//         is one DPP row_ror:8 add, followed by the two quad_perm adds.
+// A workgroup (LPP waves) owns an 8x8 block of the patch grid and stages the
 // target image region every one of its patches can sample (start +-4 px,
 // SURVEY.md 7.3 "I1 search window") into one shared LDS tile. When the block's
 // start positions are too spread for the tile, the same arithmetic reads the
@@ -42,11 +47,41 @@ constexpr int kTSMax = 96;         // max tile row stride (floats); the host pic
 // quad_perm DPP controls
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
 constexpr int kQuadXor2 = 0x4E;  // [2,3,0,1]
+constexpr int kRowRor8 = 0x128;  // row_ror:8 (lane i <-> lane i^8 within a 16-lane row)
 
 template <int CTRL>
 __device__ __forceinline__ float quad_perm(float v)
 {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// lane -> (pixel-column slot q, patch-in-block pb) for LPP lanes per patch
+template <int LPP>
+__device__ __forceinline__ void lane_map(int tid, int& q, int& pb)
+{
+    if constexpr (LPP == 8) {
+        const int w = tid & 15;
+        q = (w & 3) | ((w >> 3) << 2);
+        pb = ((tid >> 4) << 1) | ((w >> 2) & 1);
+    } else {
+        q = tid % LPP;
+        pb = tid / LPP;
+    }
+}
+
+// sum of the patch's 4 packet-accumulator lanes: (C0+C2)+(C1+C3), broadcast
+template <int LPP>
+__device__ __forceinline__ float reduce_cols(float a)
+{
+    if constexpr (LPP == 8) {
+        const float c = a + quad_perm<kRowRor8>(a);  // C_q = A_q + A_{q+4}
+        const float t = c + quad_perm<kQuadXor2>(c);
+        return t + quad_perm<kQuadXor1>(t);
+    } else {
+        static_assert(LPP == 4, "reduce_cols: LPP 4 or 8");
+        const float t = a + quad_perm<kQuadXor2>(a);  // a = C_q
+        return t + quad_perm<kQuadXor1>(t);
+    }
 }
 
 template <int LPP>
@@ -56,7 +91,7 @@ constexpr int kNCol = 8 / LPP;  // pixel columns per lane
 template <int LPP>
 __device__ __forceinline__ int lane_col(int q, int ci)
 {
-    return LPP == 4 ? q + 4 * ci : 4 * q + ci;
+    return LPP == 8 ? q : LPP == 4 ? q + 4 * ci : 4 * q + ci;
 }
 
 // Eigen-order sum of the patch's 64 values; x[ci*8 + row] holds pixel (row,
@@ -64,16 +99,19 @@ __device__ __forceinline__ int lane_col(int q, int ci)
 template <int LPP>
 __device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 {
-    if constexpr (LPP == 4) {
+    if constexpr (LPP == 8) {
+        float a = x[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) a = a + x[j];
+        return reduce_cols<8>(a);
+    } else if constexpr (LPP == 4) {
         float a = x[0];
 #pragma unroll
         for (int j = 1; j < 8; ++j) a = a + x[j];
         float b = x[8];
 #pragma unroll
         for (int j = 9; j < 16; ++j) b = b + x[j];
-        const float c = a + b;                        // C_q = A_q + A_{q+4}
-        const float t = c + quad_perm<kQuadXor2>(c);  // C_q + C_{q^2}
-        return t + quad_perm<kQuadXor1>(t);           // (C0+C2) + (C1+C3)
+        return reduce_cols<4>(a + b);  // C_q = A_q + A_{q+4}, then (C0+C2) + (C1+C3)
     } else {
         float C[4];
 #pragma unroll
@@ -92,16 +130,19 @@ __device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 template <int LPP, typename Fn>
 __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&& r)
 {
-    if constexpr (LPP == 4) {
+    if constexpr (LPP == 8) {
+        float a = g[0] * r(0);
+#pragma unroll
+        for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
+        return reduce_cols<8>(a);
+    } else if constexpr (LPP == 4) {
         float a = g[0] * r(0);
 #pragma unroll
         for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
         float b = g[8] * r(8);
 #pragma unroll
         for (int j = 9; j < 16; ++j) b = b + g[j] * r(j);
-        const float c = a + b;
-        const float t = c + quad_perm<kQuadXor2>(c);
-        return t + quad_perm<kQuadXor1>(t);
+        return reduce_cols<4>(a + b);
     } else {
         float C[4];
 #pragma unroll
@@ -152,13 +193,13 @@ __device__ __forceinline__ Warp warp_coefs(float x, float y)
 }
 
 // `tap(k, c)` returns the target image at row Y-5+k (k = 0..8) and column
-// X-5 + (LPP == 4 ? q : 4q) + c.
+// X-5 + (LPP == 2 ? 4q : q) + c.
 template <int LPP, typename Tap>
 __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[8 * kNCol<LPP>])
 {
-    if constexpr (LPP == 4) {
+    if constexpr (LPP != 2) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < kNCol<LPP>; ++s) {
             float vb[9], va[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
@@ -243,7 +284,7 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 }  // namespace
 
 template <int LPP>
-constexpr int kWaves = LPP == 4 ? DIS_SEARCH8_WAVES : 4;  // min waves per SIMD (VGPR cap 512/k)
+constexpr int kWaves = LPP == 2 ? 4 : DIS_SEARCH8_WAVES;  // min waves per SIMD (VGPR cap 512/k)
 
 // grid: (ceil(npw/8), ceil(nph/8), batch); block 64*LPP threads = 8x8 patches
 template <int LPP>
@@ -258,7 +299,8 @@ k_search8(Search8Args a)
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int q = tid % LPP, pb = tid / LPP;  // lane in patch, patch in block
+    int q, pb;  // lane's column slot in its patch, patch in block
+    lane_map<LPP>(tid, q, pb);
     const int gx = blockIdx.x * kBG + (pb >> 3);
     const int gy = blockIdx.y * kBG + (pb & 7);
     const int pair = blockIdx.z;
@@ -283,14 +325,17 @@ k_search8(Search8Args a)
     float gdx[8 * NC], gdy[8 * NC];
     if (active) {
         // NC == 2 owns columns q, q+4 (3 loads each); NC == 4 owns 4 adjacent
-        // columns sharing a 6-column window. All 60 loads are issued before
+        // columns sharing a 6-column window; NC == 1 owns column q (3 loads).
+        // All loads are issued before
         // use (a row-streamed variant that holds fewer registers measured 3%
         // slower: less memory-level parallelism in the prologue).
-        constexpr int NX = (NC == 2) ? 6 : 6;
+        constexpr int NX = (NC == 1) ? 3 : 6;
         int xs[NX];
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
-            const int col = (NC == 2) ? (irx - 4 + q + 4 * (m / 3) + (m % 3) - 1) : (irx - 5 + 4 * q + m);
+            const int col = (NC == 2)   ? (irx - 4 + q + 4 * (m / 3) + (m % 3) - 1)
+                            : (NC == 4) ? (irx - 5 + 4 * q + m)
+                                        : (irx - 5 + q + m);
             xs[m] = clampi(reflect101(col, W), 0, W - 1);
         }
         float R[NC][10], S[NC][10];
@@ -437,14 +482,14 @@ k_search8(Search8Args a)
         }
         __syncthreads();
         if (valid) {
-            const int qb = LPP == 4 ? q : 4 * q;  // lane's first tap column
+            const int qb = LPP == 2 ? 4 * q : q;  // lane's first tap column
             iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
                 return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
         }
     } else if (valid) {
-        const int qb = LPP == 4 ? q : 4 * q;
+        const int qb = LPP == 2 ? 4 * q : q;
         iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
             const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
             return [=](int k, int c) {
@@ -483,8 +528,12 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     dim3 grid((a.npw + kBG - 1) / kBG, (a.nph + kBG - 1) / kBG, batch);
     if (a.lanes_per_patch == 2)
         DIS_LAUNCH(t, k_search8<2>, grid, dim3(128), 0, s, a);
-    else
+    else if (a.lanes_per_patch == 4)
         DIS_LAUNCH(t, k_search8<4>, grid, dim3(256), 0, s, a);
+    else if (a.lanes_per_patch == 8)
+        DIS_LAUNCH(t, k_search8<8>, grid, dim3(512), 0, s, a);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -212,22 +212,22 @@ def test_golden_fixtures_on_gpu(disflow_mod, name):
 
 
 @pytest.mark.parametrize("preset", ["MEDIUM", "ULTRAFAST", "SLOW"])
-def test_four_and_two_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
-    # k_search8<2> (default) must equal k_search8<4> (variant 2) and the oracle
+def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
+    # k_search8<LPP> for LPP 2 (variant 3), 4 (variant 2) and 8 (variant 4) and
+    # the auto per-level choice (variant 0) must all equal the oracle, on the
+    # LDS-tile path and on the global-read fallback (unrelated frames)
     W, H = 352, 288
     p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
     if preset == "SLOW":
         p.iterations = 12
     I0, I1 = disflow_mod.synth_pair(77, W, H)
-    eng = disflow_mod.DenseInverseSearch(p, W, H)
-    two = eng.calc(I0, I1)
-    eng.set_variant(2)
-    four = eng.calc(I0, I1)
-    _assert_bitexact(two, four, "LPP2 vs LPP4")
-    eng.set_variant(0)
-    _assert_bitexact(two, oracle.calc_from_params(I0, I1, p), "LPP2 vs oracle")
-    # tile fallback path with LPP 2: unrelated frames
     J0, _ = disflow_mod.synth_pair(78, W, H)
     _, J1 = disflow_mod.synth_pair(79, W, H)
     J1 = np.ascontiguousarray(J1[::-1])
-    _assert_bitexact(eng.calc(J0, J1), oracle.calc_from_params(J0, J1, p), "LPP2 fallback vs oracle")
+    exp = oracle.calc_from_params(I0, I1, p)
+    exp_fb = oracle.calc_from_params(J0, J1, p)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8")):
+        eng.set_variant(variant)
+        _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
+        _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
