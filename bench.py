@@ -8,8 +8,11 @@ per GPU, launched by torch.distributed.run); there is no collective on the data
 path -- only the barrier and the max-over-ranks timing reduction.
 
 Prints ONE JSON line on rank 0 (contract in the task statement); extra fields:
-`roofline` for the dominant kernel (the patch-search kernel, all levels),
-`cpu_baseline` (the C oracle, one host core) and `max_epe_vs_oracle`.
+`roofline` for the dominant kernel (the finest-level patch-search launch,
+k_search8, ~60% of the step), which is bound by VALU issue -- its f32
+arithmetic must stay separately rounded (no FMA) to match the reference bit for
+bit -- with its HBM figures alongside; `cpu_baseline` (the C oracle, one host
+core) and `max_epe_vs_oracle`.
 """
 import argparse
 import concurrent.futures as cf
@@ -28,6 +31,10 @@ import disflow  # noqa: E402
 
 METRIC = "frame-pairs/sec at 1920x1080 preset=medium, 1/2/4/8 GPUs; max EPE vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# f32 VALU peak for non-fused operations: the 157.3 TFLOP/s vector-f32 peak
+# (MI355X_MICROARCH.md) counts an FMA as 2 FLOPs; the reference's separately
+# rounded mul/add forbid FMA, so one lane-operation per FLOP: 157.3 / 2.
+VALU_PEAK_TFLOPS = 78.6
 
 
 def parse():
@@ -112,9 +119,6 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if not a.no_kernel_timing:
-        eng.set_kernel_timing(True)
-        eng.kernel_time(disflow.KERNEL_SEARCH)  # reset accumulated records
 
     barrier()
     torch.cuda.synchronize(dev)
@@ -125,8 +129,21 @@ def main():
     barrier()
     el = time.perf_counter() - t0
 
-    n_s, ms_s = eng.kernel_time(disflow.KERNEL_SEARCH)
-    eng.set_kernel_timing(False)
+    # roofline pass (after the timed region): the same steps with the batch on
+    # one stream, so the finest-level search launch runs without co-running
+    # sub-batches; HIP dispatch events time every launch of it
+    n_f, ms_f = 0, 0.0
+    if not a.no_kernel_timing:
+        eng.set_concurrency(1)
+        step()
+        eng.set_kernel_timing(True)
+        eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)  # reset accumulated records
+        for _ in range(max(3, a.steps // 5)):
+            step()
+        torch.cuda.synchronize(dev)
+        n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
+        eng.set_kernel_timing(False)
+        eng.set_concurrency(a.streams if a.streams else 2)
     el_t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
@@ -148,17 +165,19 @@ def main():
                "sample": f"{n} synthetic {W}x{H} pairs (seeds 0..{n - 1}), preset={a.preset}, "
                          f"C oracle (oracle/dis_oracle.c, gcc -O2 -ffp-contract=off), one host thread"}
 
-    avg_ms = ms_s / max(n_s, 1)
-    # the batch runs as sub-batches on concurrent streams: bytes per launch =
-    # the step's search bytes / the step's search launches
-    launches_per_step = n_s / a.steps if n_s else wl["search_launches"]
-    bytes_per_launch = B * wl["search_bytes_all"] / launches_per_step
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if n_s else None
+    # one finest-level search launch per step in the roofline pass (B pairs)
+    avg_ms = ms_f / max(n_f, 1)
+    launches_per_step = 1
+    flops_per_launch = B * wl["search_flops_finest"] / launches_per_step
+    bytes_per_launch = B * wl["search_bytes_finest"] / launches_per_step
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if n_f else None
+    achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if n_f else None
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("batch") == B and tj.get("width") == W and tj.get("preset") == a.preset:
+            if (tj.get("batch") == B and tj.get("width") == W and tj.get("preset") == a.preset
+                    and tj.get("launches_per_step") in (None, launches_per_step)):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -183,14 +202,19 @@ def main():
                        "knobs": {"C": params.coarsest_scale, "F": params.finest_scale, "ps": params.patch_size,
                                  "it": params.iterations, "overlap": params.patch_overlap, "steps": wl["steps"]},
                        "parallelism": f"pairs sharded over {world} rank(s), no data-path collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_search (patch inverse search, all levels)",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "avg_launch_ms": avg_ms, "launches": n_s,
-                         "note": "per-launch HIP-event durations of k_search8 (one launch per level per "
-                                 "sub-batch stream; the 2 streams' launches overlap, so durations include "
-                                 "co-running time); kernel is VALU-bound, see DESIGN.md",
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "roofline": {"bound": "valu", "kernel": "k_search8, finest-level launch (patch inverse search)",
+                         "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / VALU_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                         "avg_launch_ms": avg_ms, "launches": n_f,
+                         "algorithmic_flops_per_launch": flops_per_launch,
+                         "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": (achieved_gbs / HBM_PEAK_GBS) if achieved_gbs else None,
+                                 "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "note": "bound by f32 VALU issue (bit-exact reference rounding: no FMA); "
+                                 "FLOPs = DESIGN.md 4 count x patches in the launch (all B pairs); "
+                                 "duration = HIP dispatch events of the finest-level launch in a "
+                                 "one-stream pass after the timed region; traffic = PMC HBM bytes per "
+                                 "launch of that kernel (profiles/traffic.json)"},
             "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
             "cpu_baseline": cpu,
             "max_epe_vs_oracle": max_epe,

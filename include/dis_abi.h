@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 1
+#define DIS_ABI_VERSION 2
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -77,6 +77,10 @@ typedef struct dis_workload {
     double search_bytes_all;    /* sum over search launches (levels F..C) of
                                    16*W_l*H_l + 16*n_l (+ 8*W_{l+1}*H_{l+1} coarse read) */
     int search_launches;        /* C - F + 1 */
+    long long patches_finest;   /* n_F                                          */
+    double search_flops_finest; /* algorithmic f32 operations of the finest search
+                                   for one pair: n_F * (16N - 3 + 6 + (it+1)(13N + 12))
+                                   with normalisation, N = patch_size^2 */
 } dis_workload;
 
 int dis_abi_version(void);
@@ -146,8 +150,9 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
 
 /* Kernel variant: 0 = auto (specialised kernels where available: the
  * patch_size-8 search with 8 lanes per patch on levels with few patches and 2
- * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 = the
- * patch_size-8 search with 4 / 2 / 8 lanes per patch on every level. All are
+ * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 / 5 = the
+ * patch_size-8 search with 4 / 2 / 8 / 1 lanes per patch on every level (5:
+ * where the 16x8-patch block fits, grid step <= 7; else 2). All are
  * bit-identical; the switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);

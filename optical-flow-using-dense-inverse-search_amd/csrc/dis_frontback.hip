@@ -41,6 +41,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     __shared__ float bufs1[2][(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
 
     const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < a.nzero) a.zero[tid] = 0;
     // XCD-aware tile order: the dispatcher deals linear block ids round-robin
     // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
     // and horizontally adjacent tiles share their 128-B rows in one L2.

@@ -56,7 +56,10 @@ struct Search8Args {
     float thr_sq;             // largest float s with sqrtf(s) <= outlierthresh
     int iters, norm;
     int tile_stride;          // LDS tile row stride (search8_tile_stride(steps))
-    int lanes_per_patch;      // 4 or 2 (k_search8<LPP>)
+    int lanes_per_patch;      // 1, 2, 4 or 8 (k_search8<LPP>)
+    int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
+    int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
+                              //   nullptr: one kernel with the global-read path inline
 };
 
 struct DensifyArgs {
@@ -88,6 +91,8 @@ struct PyramidArgs {
     int write_l0;  // also store the level-0 magnitude plane
     long long off[kMaxLevels];  // plane offset per level
     int w[kMaxLevels];          // plane width per level
+    int* zero;                  // nzero ints set to 0 by workgroup 0 (the searches' fallback counts)
+    int nzero;
 };
 
 // Fused densify + upsample + crop (dis_frontback.hip).
@@ -110,7 +115,8 @@ hipError_t launch_down2(const Geometry& g, int l, float* img0, float* img1, int 
 hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, float* dy, int batch,
                         hipStream_t s);
 hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s, Timing t = {});
-int search8_tile_stride(int steps);
+int search8_tile_stride(int steps, int lanes_per_patch);
+bool search8_lpp1_fits(int steps);
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);

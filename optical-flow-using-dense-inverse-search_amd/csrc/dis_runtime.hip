@@ -95,6 +95,9 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 #ifndef DIS_LPP8_MAX_PATCHES
 #define DIS_LPP8_MAX_PATCHES 65536  // level patches x pairs up to which 8 lanes/patch is used
 #endif
+#ifndef DIS_LPP_BIG
+#define DIS_LPP_BIG 2               // lanes per patch above both thresholds (1 or 2)
+#endif
 #ifndef DIS_LPP4_MAX_PATCHES
 #define DIS_LPP4_MAX_PATCHES 0      // ... and 4 lanes/patch (above: 2 lanes/patch)
 #endif
@@ -103,14 +106,16 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 // the chip idle and the level is bound by one wave's serial iteration chain:
 // spend more lanes per patch (shorter chain). Many patches make it VALU-bound:
 // 2 lanes per patch does the least total work.
-static int search8_lanes(int variant, long long patches)
+static int search8_lanes(int variant, long long patches, int steps)
 {
+    const int big = (DIS_LPP_BIG == 1 && !dis::search8_lpp1_fits(steps)) ? 2 : DIS_LPP_BIG;
     if (variant == 2) return 4;
     if (variant == 3) return 2;
     if (variant == 4) return 8;
+    if (variant == 5) return dis::search8_lpp1_fits(steps) ? 1 : 2;
     if (patches <= DIS_LPP8_MAX_PATCHES) return 8;
     if (patches <= DIS_LPP4_MAX_PATCHES) return 4;
-    return 2;
+    return big;
 }
 
 struct dis_ctx {
@@ -119,7 +124,7 @@ struct dis_ctx {
     int device = 0;
     int max_batch = 1;
     int debug = 0;
-    int variant = 0;  // 0 auto, 1 generic only, 2/3/4: patch_size-8 search with 4/2/8 lanes per patch
+    int variant = 0;  // 0 auto, 1 generic only, 2/3/4/5: patch_size-8 search with 4/2/8/1 lanes per patch
     int last_batch = 0;
     hipStream_t own = nullptr;
     static constexpr int kMaxSub = 8;
@@ -127,6 +132,7 @@ struct dis_ctx {
     hipStream_t sub[kMaxSub] = {};
     hipEvent_t fork = nullptr;
     hipEvent_t join[kMaxSub] = {};
+    hipEvent_t staged[kMaxSub] = {};  // sub-batch k's pyramid done (pipelined start of k+1)
     // workspace (device)
     float* img0 = nullptr;
     float* img1 = nullptr;
@@ -134,6 +140,11 @@ struct dis_ctx {
     float* dy = nullptr;
     float2* pu = nullptr;
     float2* dense = nullptr;
+    // patch-search fallback lists (dis_search8.hip k_search8_fb): per sub-batch
+    // k, kMaxLevels counts at fb + k * kMaxLevels, then per (k, level) a list
+    // of up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
+    int* fb = nullptr;
+    size_t fb_list_off[8][dis::kMaxLevels] = {};
     uint8_t* in0 = nullptr;  // host-mode input staging
     uint8_t* in1 = nullptr;
     float2* out = nullptr;   // host-mode output staging
@@ -184,6 +195,8 @@ void free_ws(dis_ctx* c)
     hipFree(c->dy);
     hipFree(c->pu);
     hipFree(c->dense);
+    hipFree(c->fb);
+    c->fb = nullptr;
     hipFree(c->in0);
     hipFree(c->in1);
     hipFree(c->out);
@@ -232,9 +245,11 @@ int upsample_xmax(const dis::Geometry& g)
 }
 
 // The whole path for n pairs already resident in device memory.
-dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
-                     size_t pair_stride, float2* flow, hipStream_t s)
+dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                     size_t pair_stride, float2* flow, hipStream_t s, hipEvent_t wait_pyr = nullptr,
+                     hipEvent_t pyr_done = nullptr)
 {
+    int* const fb_count = c->fb + (size_t)sub * dis::kMaxLevels;  // this sub-batch's fallback counts
     const dis::Geometry& g = c->g;
     // this sub-batch's slice of the workspace (pairs p0 .. p0+n-1)
     float* const img0 = c->img0 + (size_t)p0 * g.plane_stride;
@@ -244,6 +259,7 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
     float2* const pu = c->pu + (size_t)p0 * g.u_stride;
     float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant != 1;
+    if (wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
     {
         if (fast && g.C >= 1) {
             dis::PyramidArgs pa{};
@@ -262,13 +278,17 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
             pa.plane_stride = g.plane_stride;
             pa.levels = std::min(g.C, 6);
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
+            pa.zero = fb_count;
+            pa.nzero = g.C + 1;
             for (int l = 0; l <= g.C; ++l) {
                 pa.off[l] = g.lv[l].plane_off;
                 pa.w[l] = g.lv[l].W;
             }
             DIS_HIP(dis::launch_pyramid(pa, n, s, timing(c, 0)));
             for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
+            if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
+            if (fast) DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (g.C + 1), s));
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
             for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }
@@ -329,8 +349,10 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
             b.tmp_ub_w = L.tmp_ub_w;
             b.tmp_ub_h = L.tmp_ub_h;
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
-            b.tile_stride = dis::search8_tile_stride(L.steps);
-            b.lanes_per_patch = search8_lanes(c->variant, (long long)L.npw * L.nph * n);
+            b.lanes_per_patch = search8_lanes(c->variant, (long long)L.npw * L.nph * n, L.steps);
+            b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
+            b.fb_count = fb_count + l;
+            b.fb_list = c->fb + c->fb_list_off[sub][l];
             b.iters = g.iters;
             b.norm = g.norm;
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
@@ -418,15 +440,26 @@ dis_status run_batch(dis_ctx* c, int n, int p0, const uint8_t* I0, const uint8_t
     return DIS_OK;
 }
 
+#ifndef DIS_STAGGER
+#define DIS_STAGGER 0  // measured: lockstep sub-batches 1-3% faster on 1080p MEDIUM (search dominates)
+#endif
+#ifndef DIS_STAGGER_PRIO
+#define DIS_STAGGER_PRIO DIS_STAGGER
+#endif
+
 // Split n pairs into sub-batches on the context's streams (fork from `s`,
 // join back into `s`): pairs are independent, so the latency-bound phases of
-// one sub-batch (coarse levels, kernel tails) overlap the others' work.
+// one sub-batch (coarse levels, kernel tails) overlap the others' work. The
+// sub-batches are pipelined: sub-batch k's (HBM-bound) pyramid starts when
+// k-1's pyramid is done, so it runs beside k-1's coarse levels and search
+// (VALU-bound) instead of contending with the other pyramids for HBM, and
+// k-1's output kernel runs beside k's search.
 dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                        size_t pair_stride, float2* flow, hipStream_t s)
 {
     const int S = std::min(c->nsub, n);
     if (S <= 1) {
-        dis_status st = run_batch(c, n, 0, I0, I1, stride, pair_stride, flow, s);
+        dis_status st = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s);
         if (st == DIS_OK) c->last_batch = n;
         return st;
     }
@@ -435,8 +468,10 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     for (int k = 0; k < S; ++k) {
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
         DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
-        dis_status st = run_batch(c, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride, stride,
-                                  pair_stride, flow + (size_t)a * fpp, c->sub[k]);
+        dis_status st = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride, stride,
+                                  pair_stride, flow + (size_t)a * fpp, c->sub[k],
+                                  (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
+                                  DIS_STAGGER ? c->staged[k] : nullptr);
         if (st != DIS_OK) return st;
         DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
     }
@@ -527,6 +562,15 @@ dis_status dis_workload_info(const dis_params* params, int width, int height, di
     }
     out->search_bytes_all = sb;
     out->search_launches = g.C - g.F + 1;
+    // algorithmic f32 operations per patch (each add/sub/mul/div = 1): Sobel
+    // gradients ~10/pixel, Hessian 3 dot products, 2x2 LU; per update: bilinear
+    // warp 7/pixel (4 mul + 3 add), mean normalisation 2/pixel, 2 dot products,
+    // solve + update + outlier test ~12 (src/patch.cpp:31-267)
+    const double N = (double)g.ps * g.ps;
+    const double per_update = 7.0 * N + (g.norm ? 2.0 * N : 0.0) + 2.0 * (2.0 * N - 1.0) + 14.0;
+    const double per_patch = 10.0 * N + 3.0 * (2.0 * N - 1.0) + 6.0 + (g.iters + 1) * per_update;
+    out->patches_finest = LF.n;
+    out->search_flops_finest = (double)LF.n * per_patch;
     return DIS_OK;
 }
 
@@ -567,11 +611,34 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    if (ok) {
+        size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
+        for (int k = 0; k < dis_ctx::kMaxSub; ++k)
+            for (int l = 0; l <= g.C; ++l) {
+                c->fb_list_off[k][l] = off;
+                off += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8) * B;  // 8x8 blocks (the most)
+            }
+        ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
+             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess;
+    }
+    // pipelined sub-batches: later sub-batches get the higher priority, so the
+    // workgroups of their latency-bound coarse levels are dispatched as soon
+    // as the earlier sub-batch's search workgroups retire (not after them)
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     for (int k = 0; ok && k < dis_ctx::kMaxSub; ++k)
-        ok = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
+        ok = hipStreamCreateWithPriority(&c->sub[k], hipStreamNonBlocking,
+                                         (DIS_STAGGER_PRIO && k > 0) ? prio_hi : prio_lo) == hipSuccess &&
+             hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->staged[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         free_ws(c);
+        for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+            if (c->sub[k]) hipStreamDestroy(c->sub[k]);
+            if (c->join[k]) hipEventDestroy(c->join[k]);
+            if (c->staged[k]) hipEventDestroy(c->staged[k]);
+        }
+        if (c->fork) hipEventDestroy(c->fork);
         if (c->own) hipStreamDestroy(c->own);
         delete c;
         return fail(DIS_ERR_OUT_OF_MEMORY, "device workspace allocation failed");
@@ -591,6 +658,7 @@ dis_status dis_destroy(dis_ctx* c)
         if (c->sub[k]) hipStreamSynchronize(c->sub[k]);
         if (c->sub[k]) hipStreamDestroy(c->sub[k]);
         if (c->join[k]) hipEventDestroy(c->join[k]);
+        if (c->staged[k]) hipEventDestroy(c->staged[k]);
     }
     if (c->fork) hipEventDestroy(c->fork);
     if (c->own) hipStreamDestroy(c->own);
@@ -655,7 +723,7 @@ dis_status dis_set_concurrency(dis_ctx* c, int streams)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 4) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..4");
+    if (variant < 0 || variant > 5) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..5");
     c->variant = variant;
     return DIS_OK;
 }

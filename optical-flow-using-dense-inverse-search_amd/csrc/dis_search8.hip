@@ -9,6 +9,11 @@
 //   Patch::get_patch_second_image           src/patch.cpp:207-267.
 //
 // Mapping (CDNA4, wave64), template LPP = lanes per patch:
+//  LPP 1: 64 patches per wave, the whole patch in one lane (8 columns x 8
+//         rows): Eigen's reduction entirely in-lane (no cross-lane traffic),
+//         no per-patch scalar work duplicated across lanes, 9 shared tap
+//         columns per row; 192 VGPRs of gradients + warp, so 2 waves per SIMD.
+//         Workgroup = 2 waves on a 16x8 patch block sharing one wider tile.
 //  LPP 4: 16 patches per wave; lane q owns pixel columns q and q+4. Eigen's SSE
 //         reduction of a 64-vector (two 4-wide packet accumulators; SURVEY.md
 //         A6) is then exact:  A_c = sequential sum down column c (in-lane),
@@ -24,14 +29,22 @@
 //         idle). A patch's lanes are {4h..4h+3} and {4h+8..4h+11} of a 16-lane
 //         row (h = 0, 1), holding columns 0..3 and 4..7, so C_q = A_q + A_{q+4}
 //         is one DPP row_ror:8 add, followed by the two quad_perm adds.
-// A workgroup (LPP waves) owns an 8x8 block of the patch grid and stages the
+// A workgroup (LPP waves; 2 for LPP 1) owns a block of the patch grid and stages the
 // target image region every one of its patches can sample (start +-4 px,
 // SURVEY.md 7.3 "I1 search window") into one shared LDS tile. When the block's
 // start positions are too spread for the tile, the same arithmetic reads the
 // level plane through L1/L2 instead (identical results, slower).
+#include <algorithm>
+
 #include "dis_device.h"
 #include "dis_kernels.h"
 
+#ifndef DIS_SOBEL_FENCE
+#define DIS_SOBEL_FENCE __builtin_amdgcn_sched_barrier(0)  // rows streamed: bounded VGPRs
+#endif
+#ifndef DIS_S8_EXTRA_ATTR
+#define DIS_S8_EXTRA_ATTR
+#endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
 #endif
@@ -40,9 +53,28 @@ namespace dis {
 
 namespace {
 
-constexpr int kBG = 8;             // patch-grid block per workgroup: kBG x kBG patches
-constexpr int kTileMax = 64;       // max staged tile edge (pixels)
-constexpr int kTSMax = 96;         // max tile row stride (floats); the host picks it per grid step
+// patch-grid block per workgroup: kBX<LPP> columns x kBY rows of patches
+template <int LPP>
+constexpr int kBX = LPP == 1 ? 16 : 8;
+constexpr int kBY = 8;
+template <int LPP>
+constexpr int kThreads = kBX<LPP> * kBY * LPP;
+constexpr int kTileH = 64;  // max staged tile rows
+template <int LPP>
+constexpr int kTileW = LPP == 1 ? 96 : 64;  // max staged tile columns
+#ifndef DIS_TSMAX2
+#define DIS_TSMAX2 72  // 64 x 72-float tile (18 KB): 8 two-wave workgroups per CU = 4 waves per SIMD at LPP 2
+#endif
+template <int LPP>
+constexpr int kTSMax = LPP == 1 ? 128 : DIS_TSMAX2;  // max tile row stride (floats); the host picks it per grid step
+template <int LPP>
+constexpr int kCuMax = LPP == 1 ? 192 : 144;  // staged coarse patches (<= 16 x 12 / 12 x 12 for steps >= 1)
+template <int LPP>
+constexpr int kCuPer = (kCuMax<LPP> + kThreads<LPP> - 1) / kThreads<LPP>;  // coarse patches per thread
+#ifndef DIS_TILE_GROUP
+#define DIS_TILE_GROUP 8
+#endif
+constexpr int kTileGroup = DIS_TILE_GROUP;  // tile rows per wave in flight
 
 // quad_perm DPP controls
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
@@ -63,6 +95,9 @@ __device__ __forceinline__ void lane_map(int tid, int& q, int& pb)
         const int w = tid & 15;
         q = (w & 3) | ((w >> 3) << 2);
         pb = ((tid >> 4) << 1) | ((w >> 2) & 1);
+    } else if constexpr (LPP == 1) {
+        q = 0;
+        pb = tid;
     } else {
         q = tid % LPP;
         pb = tid / LPP;
@@ -91,7 +126,7 @@ constexpr int kNCol = 8 / LPP;  // pixel columns per lane
 template <int LPP>
 __device__ __forceinline__ int lane_col(int q, int ci)
 {
-    return LPP == 8 ? q : LPP == 4 ? q + 4 * ci : 4 * q + ci;
+    return LPP == 1 ? ci : LPP == 8 ? q : LPP == 4 ? q + 4 * ci : 4 * q + ci;
 }
 
 // Eigen-order sum of the patch's 64 values; x[ci*8 + row] holds pixel (row,
@@ -99,7 +134,16 @@ __device__ __forceinline__ int lane_col(int q, int ci)
 template <int LPP>
 __device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 {
-    if constexpr (LPP == 8) {
+    if constexpr (LPP == 1) {
+        float A[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            A[c] = x[8 * c];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) A[c] = A[c] + x[8 * c + j];
+        }
+        return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
+    } else if constexpr (LPP == 8) {
         float a = x[0];
 #pragma unroll
         for (int j = 1; j < 8; ++j) a = a + x[j];
@@ -130,7 +174,16 @@ __device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 template <int LPP, typename Fn>
 __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&& r)
 {
-    if constexpr (LPP == 8) {
+    if constexpr (LPP == 1) {
+        float A[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            A[c] = g[8 * c] * r(8 * c);
+#pragma unroll
+            for (int j = 1; j < 8; ++j) A[c] = A[c] + g[8 * c + j] * r(8 * c + j);
+        }
+        return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
+    } else if constexpr (LPP == 8) {
         float a = g[0] * r(0);
 #pragma unroll
         for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
@@ -193,11 +246,11 @@ __device__ __forceinline__ Warp warp_coefs(float x, float y)
 }
 
 // `tap(k, c)` returns the target image at row Y-5+k (k = 0..8) and column
-// X-5 + (LPP == 2 ? 4q : q) + c.
-template <int LPP, typename Tap>
+// X-5 + qb + c, qb = the lane's first pixel column (LPP 1: 0, LPP 2: 4q, else q).
+template <int LPP, bool kFence = false, typename Tap>
 __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[8 * kNCol<LPP>])
 {
-    if constexpr (LPP != 2) {
+    if constexpr (LPP == 4 || LPP == 8) {
 #pragma unroll
         for (int s = 0; s < kNCol<LPP>; ++s) {
             float vb[9], va[9];
@@ -217,16 +270,17 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
             }
         }
     } else {
-        // 5 shared tap columns, streamed row by row
-        float prev[5], cur[5];
+        // NC + 1 shared tap columns (5 for LPP 2, 9 for LPP 1), streamed row by row
+        constexpr int NC = kNCol<LPP>, NT = NC + 1;
+        float prev[NT], cur[NT];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) prev[c] = tap(0, c);
+        for (int c = 0; c < NT; ++c) prev[c] = tap(0, c);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
 #pragma unroll
-            for (int c = 0; c < 5; ++c) cur[c] = tap(j + 1, c);
+            for (int c = 0; c < NT; ++c) cur[c] = tap(j + 1, c);
 #pragma unroll
-            for (int ci = 0; ci < 4; ++ci) {
+            for (int ci = 0; ci < NC; ++ci) {
                 float t = w.w3 * cur[ci + 1];
                 t = t + w.w2 * cur[ci];
                 t = t + w.w1 * prev[ci + 1];
@@ -234,7 +288,8 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
                 r[8 * ci + j] = t;
             }
 #pragma unroll
-            for (int c = 0; c < 5; ++c) prev[c] = cur[c];
+            for (int c = 0; c < NT; ++c) prev[c] = cur[c];
+            if constexpr (kFence) __builtin_amdgcn_sched_barrier(0);  // one row of taps in flight
         }
     }
     if (norm) {
@@ -245,24 +300,28 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
 }
 
 // The per-patch iteration (src/patch.cpp:156-203) with a given tap source.
-template <int LPP, typename TapAt>
+template <int LPP, bool kFence, typename TapAt>
 __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[8 * kNCol<LPP>],
                                         const float (&gy)[8 * kNCol<LPP>], float rx, float ry, float ix, float iy,
                                         float* pu0, float* pu1, TapAt&& tap_at)
 {
     float u0 = ix, u1 = iy;
     const float sx = rx + u0, sy = ry + u1;
+    float px = sx, py = sy;
     float r[8 * kNCol<LPP>];
-    Warp w = warp_coefs(sx, sy);
-    warp_patch<LPP>(w, a.norm, tap_at(w), r);
+    // rotated loop (warp at the top): one copy of the warp code, no peeled
+    // first warp holding extra registers
     for (int counter = 1;; ++counter) {
+        const Warp w = warp_coefs(px, py);
+        warp_patch<LPP, kFence>(w, a.norm, tap_at(w), r);
         const float b0 = patch_dot<LPP>(gx, [&](int j) { return r[j]; });
         const float b1 = patch_dot<LPP>(gy, [&](int j) { return r[j]; });
         float d0, d1;
         lu2_solve(lu, b0, b1, &d0, &d1);
         u0 = u0 - d0;
         u1 = u1 - d1;
-        const float px = rx + u0, py = ry + u1;
+        px = rx + u0;
+        py = ry + u1;
         const float ex = sx - px, ey = sy - py;
         const float s2 = ex * ex + ey * ey;
         // sqrtf(s2) > outlierthresh  <=>  s2 > thr_sq (sqrt is correctly rounded
@@ -274,8 +333,6 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
             break;
         }
         if (counter > a.iters) break;
-        w = warp_coefs(px, py);
-        warp_patch<LPP>(w, a.norm, tap_at(w), r);
     }
     *pu0 = u0;
     *pu1 = u1;
@@ -283,87 +340,160 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 
 }  // namespace
 
-template <int LPP>
-constexpr int kWaves = LPP == 2 ? 4 : DIS_SEARCH8_WAVES;  // min waves per SIMD (VGPR cap 512/k)
+template <int LPP, bool kFallback>
+constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? 3 : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
 
-// grid: (ceil(npw/8), ceil(nph/8), batch); block 64*LPP threads = 8x8 patches
+// LDS of one workgroup (block of patches)
 template <int LPP>
-__global__ void __launch_bounds__(64 * LPP) __attribute__((amdgpu_waves_per_eu(kWaves<LPP>)))
-k_search8(Search8Args a)
+struct BlockLds {
+    float tile[kTileH * kTSMax<LPP>];  // the block's I0 region (gradients), then its I1 tile
+    float2 cu[kCuMax<LPP>];            // staged coarse patch displacements
+    int2 crng[kBX<LPP> + kBY];         // per block column/row: covering coarse range
+    int bnd[4];
+};
+
+// One block of patches: (bxi, byi) in units of blocks, pair index `pair`.
+// kFallback: blocks whose start positions are too spread for the LDS tile read
+// the level plane through L1/L2 (identical results); without it such a block
+// is appended to the launch's fallback list (a.fb_count / a.fb_list) for
+// k_search8_fb and nothing is written here (keeps this kernel's registers
+// low enough for 4 waves per SIMD at LPP 2).
+template <int LPP, bool kFallback>
+__device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
-    constexpr int NT = 64 * LPP, NW = LPP, NC = kNCol<LPP>;
-    __shared__ float tile[kTileMax * kTSMax];
-    __shared__ float2 cu[192];   // staged coarse patch displacements (<= 12 x 12)
-    __shared__ int2 crng[2 * 8];  // per block column/row: covering coarse range
-    __shared__ int bnd[4];
-
+    constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
+    float* const tile = S.tile;
+    float2* const cu = S.cu;
+    int2* const crng = S.crng;
+    int* const bnd = S.bnd;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     int q, pb;  // lane's column slot in its patch, patch in block
     lane_map<LPP>(tid, q, pb);
-    const int gx = blockIdx.x * kBG + (pb >> 3);
-    const int gy = blockIdx.y * kBG + (pb & 7);
-    const int pair = blockIdx.z;
+    const int st = a.steps;
+    const int bgx0 = bxi * BX, bgx1 = min(bgx0 + BX - 1, a.npw - 1);
+    const int bgy0 = byi * kBY, bgy1 = min(bgy0 + kBY - 1, a.nph - 1);
+    const int gx = bgx0 + (pb >> 3);
+    const int gy = bgy0 + (pb & 7);
     const bool active = gx < a.npw && gy < a.nph;
     const int W = a.W, H = a.H;
     const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off;
     const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off;
+    const int irx = gx * st + a.offw, iry = gy * st + a.offh;
+    const float rx = (float)irx, ry = (float)iry;
 
+    // --- 1. global loads, all issued before any is consumed: the coarse patch
+    // displacements covering the block (src/patch_grid.cpp:108-119 init) and
+    // the block's I0 region for the template gradients (every patch pixel
+    // +-1 for the Sobel taps, reflect-101 indices: src/main.cpp:34-35).
+    const int hp = 4;
+    int ga = 0, ha = 0, PH = 0, PN = 0;
+    float2 cuv[kCuPer<LPP>];
+    const float2* uc = a.u_coarse ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
+    if (uc) {
+        const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
+        const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
+        ga = max(0, floordiv(xlo - a.c_offw - hp + st, st));
+        const int gb = min(a.c_npw - 1, floordiv(xhi - a.c_offw + hp, st));
+        ha = max(0, floordiv(ylo - a.c_offh - hp + st, st));
+        const int hb = min(a.c_nph - 1, floordiv(yhi - a.c_offh + hp, st));
+        PH = hb - ha + 1;
+        PN = (gb - ga + 1) * PH;  // <= kCuMax (steps >= 1)
+#pragma unroll
+        for (int k = 0; k < kCuPer<LPP>; ++k) {
+            const int i = tid + k * NT;
+            const int cx = i / PH, cy = i - cx * PH;
+            cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
+        }
+        if (tid < BX + kBY) {
+            // covering coarse-patch range per block column / row (src/patch_grid.cpp:121-182
+            // footprint test), relative to the staged block
+            const int t = tid;
+            if (t < BX) {
+                const int x = ((bgx0 + t) * st + a.offw) >> 1;  // floor(ref.x / 2)
+                crng[t] = make_int2(max(floordiv(x - a.c_offw - hp + st, st), ga) - ga,
+                                    min(floordiv(x - a.c_offw + hp, st), gb) - ga);
+            } else {
+                const int y = ((bgy0 + t - BX) * st + a.offh) >> 1;
+                crng[t] = make_int2(max(floordiv(y - a.c_offh - hp + st, st), ha) - ha,
+                                    min(floordiv(y - a.c_offh + hp, st), hb) - ha);
+            }
+        }
+    }
+    const int x0 = bgx0 * st + a.offw - 5, y0 = bgy0 * st + a.offh - 5;
+    const int RW = (bgx1 - bgx0) * st + 10, RH = (bgy1 - bgy0) * st + 10;
+    const int RS = RW | 1;  // odd row stride
+    {
+        // 64-column strips; rows in groups of 8 per wave: 8 loads in flight
+        // per lane, bounded registers (region fits the tile buffer: host-checked)
+        for (int cs = 0; cs < RW; cs += 64) {
+            const int col = cs + lane;
+            const int c0 = clampi(reflect101(x0 + col, W), 0, W - 1);
+            for (int r0 = wave; r0 < RH; r0 += 8 * NW) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int r = r0 + NW * j;
+                    v[j] = (r < RH && col < RW) ? I0[(size_t)clampi(reflect101(y0 + r, H), 0, H - 1) * W + c0]
+                                                : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int r = r0 + NW * j;
+                    if (r < RH && col < RW) tile[r * RS + col] = v[j];
+                }
+            }
+        }
+    }
+    if (uc) {
+#pragma unroll
+        for (int k = 0; k < kCuPer<LPP>; ++k)
+            if (tid + k * NT < PN) cu[tid + k * NT] = cuv[k];
+    }
     if (tid == 0) {
         bnd[0] = 0x7fffffff;
         bnd[1] = 0x7fffffff;
         bnd[2] = -0x7fffffff;
         bnd[3] = -0x7fffffff;
     }
+    __syncthreads();
 
-    const int irx = gx * a.steps + a.offw, iry = gy * a.steps + a.offh;
-    const float rx = (float)irx, ry = (float)iry;
-
-    // --- template gradients: Sobel (ksize 3, 1/8, reflect-101) of the level
+    // --- 2. template gradients: Sobel (ksize 3, 1/8, reflect-101) of the level
     // image at pixels (rx-4+c, ry-4+j), zero outside the image (zero-padded
-    // dx/dy planes, src/main.cpp:45-47). Lane q: columns lane_col(q, ci).
+    // dx/dy planes, src/main.cpp:45-47), from the staged region, rows streamed.
+    // Lane q: columns lane_col(q, ci); region column of pixel column c is
+    // lx + 1 + c, its Sobel taps lx + c .. lx + c + 2.
     float gdx[8 * NC], gdy[8 * NC];
     if (active) {
-        // NC == 2 owns columns q, q+4 (3 loads each); NC == 4 owns 4 adjacent
-        // columns sharing a 6-column window; NC == 1 owns column q (3 loads).
-        // All loads are issued before
-        // use (a row-streamed variant that holds fewer registers measured 3%
-        // slower: less memory-level parallelism in the prologue).
-        constexpr int NX = (NC == 1) ? 3 : 6;
-        int xs[NX];
-#pragma unroll
-        for (int m = 0; m < NX; ++m) {
-            const int col = (NC == 2)   ? (irx - 4 + q + 4 * (m / 3) + (m % 3) - 1)
-                            : (NC == 4) ? (irx - 5 + 4 * q + m)
-                                        : (irx - 5 + q + m);
-            xs[m] = clampi(reflect101(col, W), 0, W - 1);
-        }
-        float R[NC][10], S[NC][10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            const int yy = clampi(reflect101(iry - 5 + k, H), 0, H - 1);
-            const float* row = I0 + (size_t)yy * W;
+        constexpr int NX = (NC == 1) ? 3 : (NC == 8) ? 10 : 6;
+        const float* reg = tile + ((gy - bgy0) * st) * RS + (gx - bgx0) * st + (NC == 2 ? q : NC == 4 ? 4 * q : q);
+        auto xoff = [](int m) { return NC == 2 ? 4 * (m / 3) + (m % 3) : m; };
+        float Rw[NC][3], Sw[NC][3];
+        auto row = [&](int k) {
             float v[NX];
 #pragma unroll
-            for (int m = 0; m < NX; ++m) v[m] = row[xs[m]];
+            for (int m = 0; m < NX; ++m) v[m] = reg[k * RS + xoff(m)];
 #pragma unroll
             for (int ci = 0; ci < NC; ++ci) {
                 const int m0 = (NC == 2) ? 3 * ci : ci;
                 const float l = v[m0], c = v[m0 + 1], rr = v[m0 + 2];
-                R[ci][k] = rr - l;
-                S[ci][k] = c * 0.25f + (l + rr) * 0.125f;
+                Rw[ci][k % 3] = rr - l;
+                Sw[ci][k % 3] = c * 0.25f + (l + rr) * 0.125f;
             }
-        }
+        };
+        row(0);
+        row(1);
 #pragma unroll
-        for (int ci = 0; ci < NC; ++ci) {
-            const int px = irx - 4 + lane_col<LPP>(q, ci);
-            const bool colin = px >= 0 && px < W;
+        for (int j = 0; j < 8; ++j) {
+            row(j + 2);
+            DIS_SOBEL_FENCE;
+            const int py = iry - 4 + j;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int py = iry - 4 + j;
-                const bool in = colin && py >= 0 && py < H;
-                const float dx = R[ci][j + 1] * 0.25f + (R[ci][j] + R[ci][j + 2]) * 0.125f;
-                const float dy = S[ci][j + 2] - S[ci][j];
+            for (int ci = 0; ci < NC; ++ci) {
+                const int px = irx - 4 + lane_col<LPP>(q, ci);
+                const bool in = px >= 0 && px < W && py >= 0 && py < H;
+                const float dx = Rw[ci][(j + 1) % 3] * 0.25f + (Rw[ci][j % 3] + Rw[ci][(j + 2) % 3]) * 0.125f;
+                const float dy = Sw[ci][(j + 2) % 3] - Sw[ci][j % 3];
                 gdx[8 * ci + j] = in ? dx : 0.0f;
                 gdy[8 * ci + j] = in ? dy : 0.0f;
             }
@@ -372,6 +502,29 @@ k_search8(Search8Args a)
 #pragma unroll
         for (int j = 0; j < 8 * NC; ++j) gdx[j] = gdy[j] = 0.0f;
     }
+
+    // --- 3. initialisation from the coarser level (src/patch_grid.cpp:108-119):
+    // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
+    // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2,
+    // gathered from the staged coarse displacements.
+    float ix = 0.0f, iy = 0.0f;
+    if (uc && active) {
+        const int2 xr = crng[gx - bgx0], yr = crng[BX + gy - bgy0];
+        float fx = 0.0f, fy = 0.0f, wt = 0.0f;
+        for (int cx = xr.x; cx <= xr.y; ++cx)
+            for (int cy = yr.x; cy <= yr.y; ++cy) {
+                const float2 v = cu[cx * PH + cy];
+                fx = fx + v.x * 0.5f;
+                fy = fy + v.y * 0.5f;
+                wt = wt + 0.5f;
+            }
+        if (wt > 0) {
+            fx = fx / wt;
+            fy = fy / wt;
+        }
+        ix = fx * 2;
+        iy = fy * 2;
+    }
     LU2 lu;
     {
         const float h00 = patch_dot<LPP>(gdx, [&](int j) { return gdx[j]; });
@@ -379,78 +532,21 @@ k_search8(Search8Args a)
         const float h11 = patch_dot<LPP>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
-
-    // --- initialisation from the coarser level (src/patch_grid.cpp:108-119):
-    // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
-    // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2.
-    // The coarse patches any patch of this block needs are staged in LDS first
-    // (one load per thread), so the gathers below are LDS reads.
-    float ix = 0.0f, iy = 0.0f;
-    if (a.u_coarse) {
-        const int st = a.steps, hp = 4;
-        const int bgx0 = blockIdx.x * kBG, bgx1 = min(bgx0 + kBG - 1, a.npw - 1);
-        const int bgy0 = blockIdx.y * kBG, bgy1 = min(bgy0 + kBG - 1, a.nph - 1);
-        const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
-        const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
-        const int ga = max(0, floordiv(xlo - a.c_offw - hp + st, st));
-        const int gb = min(a.c_npw - 1, floordiv(xhi - a.c_offw + hp, st));
-        const int ha = max(0, floordiv(ylo - a.c_offh - hp + st, st));
-        const int hb = min(a.c_nph - 1, floordiv(yhi - a.c_offh + hp, st));
-        const int PH = hb - ha + 1, PN = (gb - ga + 1) * PH;  // <= 12 x 12 (host-checked)
-        const float2* uc = a.u_coarse + (size_t)pair * a.u_stride;
-        for (int i = tid; i < PN; i += NT) {
-            const int cx = i / PH, cy = i - cx * PH;
-            cu[i] = uc[(ga + cx) * a.c_nph + ha + cy];
-        }
-        if (tid < 2 * kBG) {
-            // covering coarse-patch range per block column / row (src/patch_grid.cpp:121-182
-            // footprint test), relative to the staged block
-            const int t = tid;
-            if (t < kBG) {
-                const int x = ((bgx0 + t) * st + a.offw) >> 1;  // floor(ref.x / 2)
-                crng[t] = make_int2(max(floordiv(x - a.c_offw - hp + st, st), ga) - ga,
-                                    min(floordiv(x - a.c_offw + hp, st), gb) - ga);
-            } else {
-                const int y = ((bgy0 + t - kBG) * st + a.offh) >> 1;
-                crng[t] = make_int2(max(floordiv(y - a.c_offh - hp + st, st), ha) - ha,
-                                    min(floordiv(y - a.c_offh + hp, st), hb) - ha);
-            }
-        }
-        __syncthreads();
-        if (active) {
-            const int2 xr = crng[gx - bgx0], yr = crng[kBG + gy - bgy0];
-            const int gx0 = xr.x, gx1 = xr.y, gy0 = yr.x, gy1 = yr.y;
-            float fx = 0.0f, fy = 0.0f, wt = 0.0f;
-            for (int cx = gx0; cx <= gx1; ++cx)
-                for (int cy = gy0; cy <= gy1; ++cy) {
-                    const float2 v = cu[cx * PH + cy];
-                    fx = fx + v.x * 0.5f;
-                    fy = fy + v.y * 0.5f;
-                    wt = wt + 0.5f;
-                }
-            if (wt > 0) {
-                fx = fx / wt;
-                fy = fy / wt;
-            }
-            ix = fx * 2;
-            iy = fy * 2;
-        }
-    }
     const float sx = rx + ix, sy = ry + iy;
     const bool valid = active && !(sx < a.tmp_lb || sy < a.tmp_lb || sx > a.tmp_ub_w || sy > a.tmp_ub_h);
 
-    // --- shared tile of the target image. Every sample position p of a patch
+    // --- 4. shared tile of the target image. Every sample position p of a patch
     // satisfies |p - start| <= 4 (outlier test), so X = ceil(p + 1e-5f) lies in
     // [floor(s)-4, floor(s)+6] (the epsilon is a no-op from |p| >= 256, Q8) and
     // the taps X-5..X+3 in [floor(s)-9, floor(s)+9]; the tile takes one pixel
     // of margin on each side: [floor(s)-10, floor(s)+10] over valid patches.
+    // (The barrier below also ends every lane's reads of the I0 region.)
     {
         const int fxs = valid ? (int)floorf(sx) : 0x7fffffff;
         const int fys = valid ? (int)floorf(sy) : 0x7fffffff;
         const int fxl = valid ? (int)floorf(sx) : -0x7fffffff;
         const int fyl = valid ? (int)floorf(sy) : -0x7fffffff;
         const int m0 = wave_min(fxs), m1 = wave_min(fys), m2 = wave_max(fxl), m3 = wave_max(fyl);
-        __syncthreads();  // bnd initialised
         if (lane == 0) {
             atomicMin(&bnd[0], m0);
             atomicMin(&bnd[1], m1);
@@ -462,58 +558,109 @@ k_search8(Search8Args a)
     const bool any_valid = bnd[0] != 0x7fffffff;
     const int tx0 = bnd[0] - 10, ty0 = bnd[1] - 10;
     const int tw = bnd[2] + 10 - tx0 + 1, th = bnd[3] + 10 - ty0 + 1;
-    const bool use_tile = any_valid && tw <= kTileMax && th <= kTileMax;
+    const bool use_tile = any_valid && tw <= kTileW<LPP> && th <= kTileH;
     const int TS = a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
 
     float u0 = ix, u1 = iy;
     if (use_tile) {
-        // all of this wave's rows in flight at once, then the LDS stores
-        float v[kTileMax / NW];
-        const int cx = clampi(tx0 + lane, 0, W - 1);
+        // 64-column strips; rows in groups of kTileGroup per wave (loads in
+        // flight, then the LDS stores)
+        for (int cs = 0; cs < tw; cs += 64) {
+            const int col = cs + lane;
+            const int cx = clampi(tx0 + col, 0, W - 1);
+            for (int r0 = wave; r0 < th; r0 += kTileGroup * NW) {
+                float v[kTileGroup];
 #pragma unroll
-        for (int j = 0; j < kTileMax / NW; ++j) {
-            const int r = wave + NW * j;
-            v[j] = (r < th && lane < tw) ? I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + cx] : 0.0f;
-        }
+                for (int j = 0; j < kTileGroup; ++j) {
+                    const int r = r0 + NW * j;
+                    v[j] = (r < th && col < tw) ? I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + cx] : 0.0f;
+                }
 #pragma unroll
-        for (int j = 0; j < kTileMax / NW; ++j) {
-            const int r = wave + NW * j;
-            if (r < th && lane < tw) tile[r * TS + lane] = v[j];
+                for (int j = 0; j < kTileGroup; ++j) {
+                    const int r = r0 + NW * j;
+                    if (r < th && col < tw) tile[r * TS + col] = v[j];
+                }
+            }
         }
         __syncthreads();
         if (valid) {
-            const int qb = LPP == 2 ? 4 * q : q;  // lane's first tap column
-            iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+            const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
+            iterate<LPP, false>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
                 return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
         }
-    } else if (valid) {
-        const int qb = LPP == 2 ? 4 * q : q;
-        iterate<LPP>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
-            const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
-            return [=](int k, int c) {
-                return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
-            };
-        });
+    } else if constexpr (kFallback) {
+        if (valid) {
+            const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
+            iterate<LPP, true>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+                const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
+                return [=](int k, int c) {
+                    return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
+                };
+            });
+        }
+    } else if (any_valid) {
+        // too spread for the tile: k_search8_fb redoes this block
+        if (tid == 0) {
+            const int slot = atomicAdd(a.fb_count, 1);
+            a.fb_list[slot] = (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi;
+        }
+        return;
     }
     if (active && q == 0) a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
 }
 
-// LDS tile row stride for grid step `steps`: the 8 vertically adjacent patches
-// of a half-wave (4 lanes each) sit steps*S floats apart; pick S in
-// [kTileMax+1, kTSMax] minimising the worst bank multiplicity of
-// (steps*S*g + q) mod 32, g < 8, q < 4 (ds_read_b32 banking, 32-lane groups).
-int search8_tile_stride(int steps)
+// grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
+template <int LPP, bool kFallback>
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
+k_search8(Search8Args a)
 {
-    int best = kTileMax + 1, best_m = 1 << 30;
-    for (int S = kTileMax + 1; S <= kTSMax; ++S) {
+    __shared__ BlockLds<LPP> S;
+    search_block<LPP, kFallback>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+}
+
+// The blocks k_search8<LPP, false> listed: persistent workgroups over the list
+// (usually empty: every workgroup reads the count and exits).
+template <int LPP>
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, true>)))
+k_search8_fb(Search8Args a)
+{
+    __shared__ BlockLds<LPP> S;
+    const int n = *a.fb_count;
+    const int nbx = (a.npw + kBX<LPP> - 1) / kBX<LPP>, nby = (a.nph + kBY - 1) / kBY;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int e = a.fb_list[i];
+        const int bx = e % nbx, t = e / nbx;
+        search_block<LPP, true>(a, bx, t % nby, t / nby, S);
+        __syncthreads();  // LDS reuse by the next listed block
+    }
+}
+
+// LDS tile row stride for grid step `steps` and lane layout LPP: the
+// patches of one 32-lane LDS group sit at (steps*S*gy + steps*gx + lane column
+// offset) floats for zero flow; pick S in [tile width + 1, kTSMax] minimising
+// the worst bank multiplicity ((a/4) mod 32, ds_read_b32 banking).
+int search8_tile_stride(int steps, int lpp)
+{
+    const int w = lpp == 1 ? kTileW<1> : kTileW<2>, smax = lpp == 1 ? kTSMax<1> : kTSMax<2>;
+    int best = w + 1, best_m = 1 << 30;
+    for (int S = w + 1; S <= smax; ++S) {
         int cnt[32] = {0}, m = 0;
-        for (int g = 0; g < 8; ++g)
-            for (int q = 0; q < 4; ++q) {
-                const int b = (int)(((long long)steps * S * g + q) % 32);
-                m = ++cnt[b] > m ? cnt[b] : m;
+        for (int l = 0; l < 32; ++l) {
+            int gx, gy, off;
+            if (lpp == 1) {  // lane = patch: gx = l / 8, gy = l % 8
+                gx = l >> 3, gy = l & 7, off = 0;
+            } else if (lpp == 2) {  // 16 patches x 2 lanes (4 columns apart)
+                gx = (l >> 1) >> 3, gy = (l >> 1) & 7, off = 4 * (l & 1);
+            } else if (lpp == 4) {  // 8 patches x 4 lanes
+                gx = 0, gy = l >> 2, off = l & 3;
+            } else {  // lpp 8: 4 patches x 8 lanes
+                gx = 0, gy = (l >> 4) * 2 + ((l >> 2) & 1), off = (l & 3) | (((l >> 3) & 1) << 2);
             }
+            const int b = (int)(((long long)steps * S * gy + steps * gx + off) % 32);
+            m = ++cnt[b] > m ? cnt[b] : m;
+        }
         if (m < best_m) {
             best_m = m;
             best = S;
@@ -522,18 +669,44 @@ int search8_tile_stride(int steps)
     return best;
 }
 
+// Whether the LPP-1 layout fits: the 16x8 block's I0 region must fit its tile buffer.
+bool search8_lpp1_fits(int steps)
+{
+    return (15 * steps + 11) * (7 * steps + 10) <= kTileH * kTSMax<1>;
+}
+
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t)
 {
-    if (a.tile_stride < kTileMax + 1 || a.tile_stride > kTSMax) return hipErrorInvalidValue;
-    dim3 grid((a.npw + kBG - 1) / kBG, (a.nph + kBG - 1) / kBG, batch);
-    if (a.lanes_per_patch == 2)
-        DIS_LAUNCH(t, k_search8<2>, grid, dim3(128), 0, s, a);
-    else if (a.lanes_per_patch == 4)
-        DIS_LAUNCH(t, k_search8<4>, grid, dim3(256), 0, s, a);
-    else if (a.lanes_per_patch == 8)
-        DIS_LAUNCH(t, k_search8<8>, grid, dim3(512), 0, s, a);
-    else
-        return hipErrorInvalidValue;
+    const int L = a.lanes_per_patch;
+    if (L != 1 && L != 2 && L != 4 && L != 8) return hipErrorInvalidValue;
+    const int w = L == 1 ? kTileW<1> : kTileW<2>, smax = L == 1 ? kTSMax<1> : kTSMax<2>;
+    if (a.tile_stride < w + 1 || a.tile_stride > smax) return hipErrorInvalidValue;
+    if (L == 1 && !search8_lpp1_fits(a.steps)) return hipErrorInvalidValue;
+    if (L != 1 && (7 * a.steps + 11) * (7 * a.steps + 10) > kTileH * kTSMax<2>) return hipErrorInvalidValue;
+    const int bx = L == 1 ? kBX<1> : kBX<2>;
+    dim3 grid((a.npw + bx - 1) / bx, (a.nph + kBY - 1) / kBY, batch);
+    const bool split = (L == 1 || L == 2) && a.fb_count && a.fb_list;
+    // persistent fallback workgroups: enough for a few listed blocks per CU
+    const dim3 fb_grid(std::min<long long>(512, (long long)grid.x * grid.y * grid.z));
+    if (L == 1) {
+        if (split) {
+            DIS_LAUNCH(t, (k_search8<1, false>), grid, dim3(kThreads<1>), 0, s, a);
+            hipLaunchKernelGGL(k_search8_fb<1>, fb_grid, dim3(kThreads<1>), 0, s, a);
+        } else {
+            DIS_LAUNCH(t, (k_search8<1, true>), grid, dim3(kThreads<1>), 0, s, a);
+        }
+    } else if (L == 2) {
+        if (split) {
+            DIS_LAUNCH(t, (k_search8<2, false>), grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL(k_search8_fb<2>, fb_grid, dim3(kThreads<2>), 0, s, a);
+        } else {
+            DIS_LAUNCH(t, (k_search8<2, true>), grid, dim3(kThreads<2>), 0, s, a);
+        }
+    } else if (L == 4) {
+        DIS_LAUNCH(t, (k_search8<4, true>), grid, dim3(kThreads<4>), 0, s, a);
+    } else {
+        DIS_LAUNCH(t, (k_search8<8, true>), grid, dim3(kThreads<8>), 0, s, a);
+    }
     return hipGetLastError();
 }
 

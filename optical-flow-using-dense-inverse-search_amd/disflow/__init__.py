@@ -95,6 +95,8 @@ class _Workload(ctypes.Structure):
         ("search_bytes_finest", ctypes.c_double),
         ("search_bytes_all", ctypes.c_double),
         ("search_launches", ctypes.c_int),
+        ("patches_finest", ctypes.c_longlong),
+        ("search_flops_finest", ctypes.c_double),
     ]
 
 

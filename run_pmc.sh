@@ -1,16 +1,25 @@
 #!/bin/bash
-# PMC counter passes (each its own rocprofv3 run; no tracing domains combined).
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-TAG=${TAG:-pmc}
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > "$GRAFT_REPO_ROOT/gpurun_out/counters_list.txt" 2>&1
-echo "list rc=$?"
-i=0
-for set in "$@"; do
-  i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_$i.log" 2>&1
-  rc=$?
-  echo "pass $i ($set) rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_$i.log"; exit $rc; fi
+# SQ counters per (kernel, grid) for tools/ab.py "$1" (one variant), top kernels
+cd "$GRAFT_REPO_ROOT"; R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+CTRS=${CTRS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}
+k=0
+for v in "$@"; do
+  k=$((k+1))
+  timeout -k 10 90 rocprofv3 --pmc $CTRS --output-format csv -d $R/gpurun_out/pmc_$k -o run -- python3 $R/tools/ab.py $v --rounds 1 --steps 2 > $R/gpurun_out/pmc_$k.log 2>&1 || { tail -5 $R/gpurun_out/pmc_$k.log; exit 1; }
+  echo "== $v"
+  (cd $R && python3 - gpurun_out/pmc_$k/run_counter_collection.csv <<'PY'
+import csv, collections, sys
+agg = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.defaultdict(set)
+for r in csv.DictReader(open(sys.argv[1])):
+    k = (r['Kernel_Name'][:26], int(r['Grid_Size']))
+    agg[k][r['Counter_Name']] += float(r['Counter_Value']); n[k].add(r['Dispatch_Id'])
+for k, c in sorted(agg.items(), key=lambda kv: -kv[1]['SQ_INSTS_VALU'])[:3]:
+    m = len(n[k]); w = c['SQ_WAVES'] / m
+    d = {x: v / m for x, v in c.items()}
+    print(k, ' '.join(f"{x}={v:.4g}" for x, v in d.items()))
+    print('   per wave: VALU %.0f LDS %.0f  wave-cycles %.0f  wait %.0f  bankconf/LDS %.2f' % (
+        d["SQ_INSTS_VALU"] / w, d['SQ_INSTS_LDS'] / w, d['SQ_WAVE_CYCLES'] / w,
+        d.get('SQ_WAIT_INST_ANY', 0) / w, d.get('SQ_LDS_BANK_CONFLICT', 0) / max(d['SQ_INSTS_LDS'], 1)))
+PY
+)
 done

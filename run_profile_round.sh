@@ -13,5 +13,5 @@ run write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/${TAG}
 run sq rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/${TAG}_sq -o run -- python3 $BENCH
 cd $R
 python3 tools/pmc_traffic.py gpurun_out/${TAG}_fetch/run_counter_collection.csv gpurun_out/${TAG}_write/run_counter_collection.csv --out gpurun_out/traffic.json
-cat gpurun_out/${TAG}_trace/run_kernel_stats.csv | cut -c1-200
+python3 tools/trace_stats.py gpurun_out/${TAG}_trace/run_kernel_trace.csv gpurun_out/${TAG}_trace/kernel_grid_stats.csv
 timeout -k 10 400 python3 bench.py --traffic-json gpurun_out/traffic.json > gpurun_out/bench_final.log 2>&1; echo "bench rc=$?"; tail -1 gpurun_out/bench_final.log

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(disflow_mod):
     L = disflow_mod.lib()
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert L.dis_abi_version() == 1
+    assert L.dis_abi_version() == 2
 
 
 def test_no_oracle_linked_into_product(disflow_mod):
@@ -88,6 +88,8 @@ def test_workload_medium_1080p(disflow_mod):
     assert (w["padded_width"], w["padded_height"], w["steps"]) == (1920, 1088, 3)
     assert w["patches"] == 77700
     assert w["updates"] == 2020200
+    assert w["patches_finest"] == 320 * 182
+    assert w["search_flops_finest"] == 58240 * (1027 + 26 * 844)  # per patch / per update
     assert abs(w["algorithmic_bytes"] / 1e6 - 72.11) < 0.01
     u = disflow_mod.workload(disflow_mod.preset_params(disflow_mod.Preset.ULTRAFAST, 640, 480), 640, 480)
     assert u["patches"] == 1580 and u["updates"] == 20540

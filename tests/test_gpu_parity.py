@@ -213,7 +213,7 @@ def test_golden_fixtures_on_gpu(disflow_mod, name):
 
 @pytest.mark.parametrize("preset", ["MEDIUM", "ULTRAFAST", "SLOW"])
 def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
-    # k_search8<LPP> for LPP 2 (variant 3), 4 (variant 2) and 8 (variant 4) and
+    # k_search8<LPP> for LPP 2 (variant 3), 4 (variant 2), 8 (variant 4), 1 (variant 5) and
     # the auto per-level choice (variant 0) must all equal the oracle, on the
     # LDS-tile path and on the global-read fallback (unrelated frames)
     W, H = 352, 288
@@ -227,7 +227,7 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
     exp = oracle.calc_from_params(I0, I1, p)
     exp_fb = oracle.calc_from_params(J0, J1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8")):
+    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1")):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")

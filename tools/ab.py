@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of library builds in ONE process (cdna guide §5.4
 rule 24): each variant = path to a libdis_hip*.so [+ ":streams=N"]; rounds
-alternate variants; prints median/min ms per step and pairs/s per variant."""
+alternate variants; prints median/min ms per step and pairs/s per variant.
+
+--spawn N: instead, N rounds of one child process per variant (interleaved),
+for variants whose streams would interfere inside one process (several
+contexts' streams share the process's hardware queues)."""
 import argparse
 import ctypes
 import os
@@ -26,7 +30,10 @@ def main():
     ap.add_argument("--preset", default="medium")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spawn", type=int, default=0)
     a = ap.parse_args()
+    if a.spawn:
+        return spawn(a)
     W, H, B = a.width, a.height, a.batch
     dev = torch.device("cuda", 0)
     pairs = [disflow.synth_pair(k, W, H) for k in range(B)]
@@ -39,9 +46,11 @@ def main():
         disflow.LIB_PATH = os.path.join(ROOT, path) if not os.path.isabs(path) else path
         L = disflow.lib()
         p = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
+        opts = dict(kv.partition("=")[::2] for kv in filter(None, opt.split(",")))
+        if "iters" in opts:
+            p.iterations = int(opts.pop("iters"))
         eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
-        for kv in filter(None, opt.split(",")):
-            k, _, val = kv.partition("=")
+        for k, val in opts.items():
             if k == "streams":
                 eng.set_concurrency(int(val))
             elif k == "variant":
@@ -68,6 +77,25 @@ def main():
         t = times[v]
         print(f"{v:70s} median {statistics.median(t):.3f} ms  min {min(t):.3f} ms  "
               f"pairs/s {B / statistics.median(t) * 1e3:.0f}  same_as_first={same}")
+
+
+def spawn(a):
+    import re
+    import subprocess
+    res = {v: [] for v in a.variants}
+    for _ in range(a.spawn):
+        for v in a.variants:
+            cmd = [sys.executable, os.path.abspath(__file__), v, "--rounds", str(a.rounds), "--steps", str(a.steps),
+                   "--batch", str(a.batch), "--preset", a.preset, "--width", str(a.width), "--height", str(a.height)]
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(out.stdout, out.stderr, file=sys.stderr)
+                raise SystemExit(f"child failed: {v}")
+            m = re.search(r"median ([0-9.]+) ms", out.stdout)
+            res[v].append(float(m.group(1)))
+    for v, t in res.items():
+        print(f"{v:70s} median-of-process-medians {statistics.median(t):.3f} ms  min {min(t):.3f} ms  "
+              f"pairs/s {a.batch / statistics.median(t) * 1e3:.0f}  ({len(t)} processes)")
 
 
 if __name__ == "__main__":

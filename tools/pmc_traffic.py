@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a bench.py run into HBM
-bytes per launch per kernel, and write the search kernel's figure to
+bytes per launch per kernel (and launch grid), and write the finest-level
+search launch's figure (the k_search8 launch with the largest grid) to
 profiles/traffic.json (read by bench.py as `roofline.traffic`).
 
 Correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE on gfx950 counts
@@ -20,7 +21,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"]
+        k = f'{r["Kernel_Name"]} grid={r["Grid_Size"]}'
         tot[k] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     return {k: (tot[k] / len(disp[k]), len(disp[k])) for k in tot}
@@ -44,16 +45,16 @@ def main():
         wk, _ = w.get(k, (0.0, 0))
         kernels[k] = {"launches": n, "fetch_kib": fk, "write_kib": wk,
                       "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-    search = [k for k in kernels if "k_search8" in k]
+    search = sorted((k for k in kernels if "k_search8" in k), key=lambda k: -int(k.rsplit("=", 1)[1]))
     out = {"batch": a.batch, "width": a.width, "height": a.height, "preset": a.preset,
-           "kernel": search[0] if search else None,
+           "kernel": (search[0] + " (finest level)") if search else None,
            "hbm_bytes_per_launch": kernels[search[0]]["hbm_bytes_per_launch"] if search else None,
            "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half the bytes; "
                          "calibrated with tools/pmc_calib for 1/4/16-B loads)",
            "kernels": kernels}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in kernels.items():
-        print(f"{k[:60]:60s} launches {v['launches']:3d}  HBM MB/launch {v['hbm_bytes_per_launch'] / 1e6:9.2f}")
+        print(f"{k[:72]:72s} launches {v['launches']:3d}  HBM MB/launch {v['hbm_bytes_per_launch'] / 1e6:9.2f}")
 
 
 if __name__ == "__main__":
