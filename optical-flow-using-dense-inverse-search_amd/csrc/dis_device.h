@@ -93,4 +93,21 @@ __device__ __forceinline__ float2 dense_at(const float2* __restrict__ u, int npw
     return make_float2(fx, fy);
 }
 
+// Correctly rounded sqrt for x = 0 or a normal float well inside the range
+// (no denormal pre-scaling): v_sqrt_f32 is within one ulp; the fma residuals
+// of the neighbours r -/+ 1 ulp pick the rounded root. Used by the pyramid on
+// x = N, an integer < 2^22 (Sobel magnitude^2 * 64); tools/sqrt_check proves
+// it equal to sqrtf on every such N on gfx950 (the raw v_sqrt_f32 is not).
+__device__ __forceinline__ float sqrt_cr(float x)
+{
+    const float r = __builtin_amdgcn_sqrtf(x);
+    const float rm = __int_as_float(__float_as_int(r) - 1);
+    const float rp = __int_as_float(__float_as_int(r) + 1);
+    const float em = __builtin_fmaf(-rm, r, x);
+    const float ep = __builtin_fmaf(-rp, r, x);
+    float y = em <= 0.0f ? rm : r;
+    y = ep > 0.0f ? rp : y;
+    return y;
+}
+
 }  // namespace dis

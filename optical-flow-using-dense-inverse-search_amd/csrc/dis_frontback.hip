@@ -50,7 +50,10 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
     const int per = nb / 8;
     const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
-    const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
+    // (divisions run on the vector unit: make the results provably uniform)
+    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
+    const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
     const int tx = bx * T0, ty = by * T0;
     const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
 
@@ -59,7 +62,8 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     // loads rows w, w+4, ...; the row offset is wave-uniform (scalar unit), the
     // column index is computed once per lane.
     {
-        const int lane = tid & 63, wave = tid >> 6;
+        // wave index made provably uniform: the row arithmetic below runs on the scalar unit
+        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         constexpr int NWV = kPyrT / 64, NR = (SS + NWV - 1) / NWV;  // rows per wave
         const int c0 = lane, c1 = lane + 64;
         const int xs0 = clampi(reflect101(tx - 1 + c0, a.Wp) - a.pl, 0, a.W - 1);
@@ -72,7 +76,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
             for (int j = 0; j < NR; ++j) {
                 const int r = wave + NWV * j;
                 const int ys = clampi(reflect101(ty - 1 + min(r, SS - 1), a.Hp) - a.pt, 0, a.H - 1);
-                const uint8_t* row = in + (size_t)__builtin_amdgcn_readfirstlane(ys) * a.stride;
+                const uint8_t* row = in + (size_t)ys * a.stride;
                 v0[f][j] = (c0 < SS) ? row[xs0] : 0;
                 v1[f][j] = (c1 < SS) ? row[xs1] : 0;
             }
@@ -107,16 +111,21 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
         const int k = k0 + tid;
         if (NB * NB % kPyrT != 0 && k >= NB * NB) break;
         const int by = k / NB, bx = k - by * NB;
-        float R[E0 + 2][E0], S[E0 + 2][E0];
+        // Sobel in exact integer arithmetic: with u8 input, R = r - l and
+        // T = 2c + l + r are integers, gx = (2R1 + R0 + R2) / 8 and
+        // gy = (T2 - T0) / 8 exactly (the reference's float expressions have
+        // no rounding here), so gx^2 + gy^2 = N / 64 exactly for the integer
+        // N = k1^2 + k2^2 < 2^21, and sqrtf(N / 64) = sqrt_cr(N) / 8.
+        int R[E0 + 2][E0], T[E0 + 2][E0];
 #pragma unroll
         for (int r = 0; r < E0 + 2; ++r) {
-            float v[E0 + 2];
+            int v[E0 + 2];
 #pragma unroll
-            for (int c = 0; c < E0 + 2; ++c) v[c] = (float)src[(E0 * by + r) * SS + E0 * bx + c];
+            for (int c = 0; c < E0 + 2; ++c) v[c] = src[(E0 * by + r) * SS + E0 * bx + c];
 #pragma unroll
             for (int c = 0; c < E0; ++c) {
                 R[r][c] = v[c + 2] - v[c];
-                S[r][c] = v[c + 1] * 0.25f + (v[c] + v[c + 2]) * 0.125f;
+                T[r][c] = 2 * v[c + 1] + v[c] + v[c + 2];
             }
         }
         float m[E0][E0];
@@ -124,19 +133,18 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
         for (int r = 0; r < E0; ++r)
 #pragma unroll
             for (int c = 0; c < E0; ++c) {
-                const float gx = R[r + 1][c] * 0.25f + (R[r][c] + R[r + 2][c]) * 0.125f;
-                const float gy = S[r + 2][c] - S[r][c];
-                const float t1 = gx * gx, t2 = gy * gy;
-                const float s = t1 + t2;
-                m[r][c] = sqrtf(s);
+                const int k1 = 2 * R[r + 1][c] + R[r][c] + R[r + 2][c];
+                const int k2 = T[r + 2][c] - T[r][c];
+                m[r][c] = sqrt_cr((float)(k1 * k1 + k2 * k2)) * 0.125f;
             }
         if (a.write_l0) {
+            float* const p0 = planes + (size_t)ty * a.Wp + tx;  // uniform base, 32-bit lane offsets
 #pragma unroll
             for (int r = 0; r < E0; ++r)
 #pragma unroll
-                for (int c = 0; c < E0; ++c)
-                    planes[(size_t)(ty + E0 * by + r) * a.Wp + tx + E0 * bx + c] = m[r][c];
+                for (int c = 0; c < E0; ++c) p0[(E0 * by + r) * a.Wp + E0 * bx + c] = m[r][c];
         }
+        float* const p1 = planes + a.off[1] + (size_t)(ty / 2) * a.w[1] + tx / 2;
 #pragma unroll
         for (int i = 0; i < B1; ++i)
 #pragma unroll
@@ -147,7 +155,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 const float l1 = s * 0.25f;
                 const int y1 = B1 * by + i, x1 = B1 * bx + j;
                 buf0[y1 * N1 + x1] = l1;
-                planes[a.off[1] + (size_t)(ty / 2 + y1) * a.w[1] + tx / 2 + x1] = l1;
+                p1[y1 * a.w[1] + x1] = l1;
             }
     }
 
@@ -158,6 +166,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     for (int l = 2; l <= LEVELS; ++l) {
         __syncthreads();
         const int ns = T0 >> (l - 1), nd = ns / 2;
+        float* const pl = planes + a.off[l] + (size_t)(ty >> l) * a.w[l] + (tx >> l);
         for (int k = tid; k < nd * nd; k += kPyrT) {
             const int y = k / nd, x = k - y * nd;
             const float* p = cur + (2 * y) * ns + 2 * x;
@@ -166,7 +175,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
             s = s + p[ns + 1];
             const float v = s * 0.25f;
             nxt[k] = v;
-            planes[a.off[l] + (size_t)((ty >> l) + y) * a.w[l] + (tx >> l) + x] = v;
+            pl[y * a.w[l] + x] = v;
         }
         float* t = cur;
         cur = nxt;

@@ -231,3 +231,16 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
+
+
+@pytest.mark.gpu
+def test_pyramid_sqrt_is_correctly_rounded_on_every_input():
+    # k_pyramid takes the Sobel magnitude as sqrt_cr(N) / 8 (N = 64 * (gx^2 + gy^2),
+    # an integer < 2^21 for u8 input); tools/sqrt_check compares it with the
+    # correctly rounded sqrtf for every possible N on this GPU
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "sqrt_check")
+    assert os.path.exists(exe), "tools/sqrt_check not built (__graft_entry__.build)"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "sqrt_cr: 0 mismatches" in out.stdout, out.stdout + out.stderr
