@@ -367,7 +367,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     int2* const crng = S.crng;
     int* const bnd = S.bnd;
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave: scalar row math
     int q, pb;  // lane's column slot in its patch, patch in block
     lane_map<LPP>(tid, q, pb);
     const int st = a.steps;
