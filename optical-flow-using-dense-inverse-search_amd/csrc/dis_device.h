@@ -18,6 +18,15 @@ __device__ __forceinline__ int reflect101(int i, int n)
 
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
+// floor(a / b) for a positive integer b given rb = v_rcp_f32(b) (<= 1 ulp):
+// (a + 0.5) / b sits >= 0.5 / b away from every integer, and the float error
+// of (a + 0.5) * rb is < |a| / b * 2^-22, so the floor is exact for
+// |a| < 2^20. Replaces the ~15-instruction integer division sequence.
+__device__ __forceinline__ int floordiv_r(int a, float rb)
+{
+    return (int)floorf(((float)a + 0.5f) * rb);
+}
+
 // Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
 // (src/patch.cpp:176): pivot on |a10| > |a00| (first index wins ties),
 // l = a_q0 / a_p0 (skipped when the pivot is 0), u11 = a_q1 - l * a_p1.

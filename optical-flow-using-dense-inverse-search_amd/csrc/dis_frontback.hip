@@ -284,8 +284,9 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const int rw = i1 - i0 + 1, rh = j1 - j0 + 1;
     // patches whose footprint meets the window
     const int st = a.steps, hp = a.hp;
-    const int ga = max(0, floordiv(i0 - a.offw - hp + st, st)), gb = min(a.npw - 1, floordiv(i1 - a.offw + hp, st));
-    const int ha = max(0, floordiv(j0 - a.offh - hp + st, st)), hb = min(a.nph - 1, floordiv(j1 - a.offh + hp, st));
+    const float rst = __builtin_amdgcn_rcpf((float)st);
+    const int ga = max(0, floordiv_r(i0 - a.offw - hp + st, rst)), gb = min(a.npw - 1, floordiv_r(i1 - a.offw + hp, rst));
+    const int ha = max(0, floordiv_r(j0 - a.offh - hp + st, rst)), hb = min(a.nph - 1, floordiv_r(j1 - a.offh + hp, rst));
     const int PW = gb - ga + 1, PH = hb - ha + 1;  // <= kOutPX x kOutPY (output_fits)
     {
         constexpr int NL = (kOutPX * kOutPY + 255) / 256;
@@ -304,13 +305,13 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     // covering patch ranges per window column / row (one floordiv pair each)
     if (tid < rw) {
         const int px = i0 + tid;
-        cr[tid] = make_int2(max(floordiv(px - a.offw - hp + st, st), ga) - ga,
-                            min(floordiv(px - a.offw + hp, st), gb) - ga);
+        cr[tid] = make_int2(max(floordiv_r(px - a.offw - hp + st, rst), ga) - ga,
+                            min(floordiv_r(px - a.offw + hp, rst), gb) - ga);
     }
     if (tid >= 128 && tid - 128 < rh) {
         const int py = j0 + tid - 128;
-        rr[tid - 128] = make_int2(max(floordiv(py - a.offh - hp + st, st), ha) - ha,
-                                  min(floordiv(py - a.offh + hp, st), hb) - ha);
+        rr[tid - 128] = make_int2(max(floordiv_r(py - a.offh - hp + st, rst), ha) - ha,
+                                  min(floordiv_r(py - a.offh + hp, rst), hb) - ha);
     }
     __syncthreads();
     const float sc = a.sc;

@@ -393,16 +393,18 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     if (uc) {
         const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
         const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
-        ga = max(0, floordiv(xlo - a.c_offw - hp + st, st));
-        const int gb = min(a.c_npw - 1, floordiv(xhi - a.c_offw + hp, st));
-        ha = max(0, floordiv(ylo - a.c_offh - hp + st, st));
-        const int hb = min(a.c_nph - 1, floordiv(yhi - a.c_offh + hp, st));
+        const float rst = __builtin_amdgcn_rcpf((float)st);
+        ga = max(0, floordiv_r(xlo - a.c_offw - hp + st, rst));
+        const int gb = min(a.c_npw - 1, floordiv_r(xhi - a.c_offw + hp, rst));
+        ha = max(0, floordiv_r(ylo - a.c_offh - hp + st, rst));
+        const int hb = min(a.c_nph - 1, floordiv_r(yhi - a.c_offh + hp, rst));
         PH = hb - ha + 1;
         PN = (gb - ga + 1) * PH;  // <= kCuMax (steps >= 1)
+        const float rph = __builtin_amdgcn_rcpf((float)PH);
 #pragma unroll
         for (int k = 0; k < kCuPer<LPP>; ++k) {
             const int i = tid + k * NT;
-            const int cx = i / PH, cy = i - cx * PH;
+            const int cx = floordiv_r(i, rph), cy = i - cx * PH;
             cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
         }
         if (tid < BX + kBY) {
@@ -411,12 +413,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             const int t = tid;
             if (t < BX) {
                 const int x = ((bgx0 + t) * st + a.offw) >> 1;  // floor(ref.x / 2)
-                crng[t] = make_int2(max(floordiv(x - a.c_offw - hp + st, st), ga) - ga,
-                                    min(floordiv(x - a.c_offw + hp, st), gb) - ga);
+                crng[t] = make_int2(max(floordiv_r(x - a.c_offw - hp + st, rst), ga) - ga,
+                                    min(floordiv_r(x - a.c_offw + hp, rst), gb) - ga);
             } else {
                 const int y = ((bgy0 + t - BX) * st + a.offh) >> 1;
-                crng[t] = make_int2(max(floordiv(y - a.c_offh - hp + st, st), ha) - ha,
-                                    min(floordiv(y - a.c_offh + hp, st), hb) - ha);
+                crng[t] = make_int2(max(floordiv_r(y - a.c_offh - hp + st, rst), ha) - ha,
+                                    min(floordiv_r(y - a.c_offh + hp, rst), hb) - ha);
             }
         }
     }
