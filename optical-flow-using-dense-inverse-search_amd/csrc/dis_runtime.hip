@@ -93,7 +93,7 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 // context
 // ---------------------------------------------------------------------------
 #ifndef DIS_LPP8_MAX_PATCHES
-#define DIS_LPP8_MAX_PATCHES 65536  // level patches x pairs up to which 8 lanes/patch is used
+#define DIS_LPP8_MAX_PATCHES 16384  // level patches x pairs up to which 8 lanes/patch is used (A/B: 65536 -2.6%)
 #endif
 #ifndef DIS_LPP_BIG
 #define DIS_LPP_BIG 2               // lanes per patch above both thresholds (1 or 2)
