@@ -71,6 +71,9 @@ template <int LPP>
 constexpr int kCuMax = LPP == 1 ? 192 : 144;  // staged coarse patches (<= 16 x 12 / 12 x 12 for steps >= 1)
 template <int LPP>
 constexpr int kCuPer = (kCuMax<LPP> + kThreads<LPP> - 1) / kThreads<LPP>;  // coarse patches per thread
+#ifndef DIS_FB_WGS
+#define DIS_FB_WGS 256
+#endif
 #ifndef DIS_TILE_GROUP
 #define DIS_TILE_GROUP 8
 #endif
@@ -624,8 +627,12 @@ k_search8(Search8Args a)
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
 // (usually empty: every workgroup reads the count and exits).
+// Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
+// its workgroups cannot take the slots another stream's search kernel frees,
+// and the (usually empty) launch waited 70-150 us for that kernel to drain.
 template <int LPP>
-__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, true>)))
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
+__attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
@@ -688,8 +695,8 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     const int bx = L == 1 ? kBX<1> : kBX<2>;
     dim3 grid((a.npw + bx - 1) / bx, (a.nph + kBY - 1) / kBY, batch);
     const bool split = (L == 1 || L == 2) && a.fb_count && a.fb_list;
-    // persistent fallback workgroups: enough for a few listed blocks per CU
-    const dim3 fb_grid(std::min<long long>(512, (long long)grid.x * grid.y * grid.z));
+    // persistent fallback workgroups (grid-stride over the list), one per CU
+    const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
     if (L == 1) {
         if (split) {
             DIS_LAUNCH(t, (k_search8<1, false>), grid, dim3(kThreads<1>), 0, s, a);
