@@ -244,3 +244,32 @@ def test_pyramid_sqrt_is_correctly_rounded_on_every_input():
     assert os.path.exists(exe), "tools/sqrt_check not built (__graft_entry__.build)"
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and "sqrt_cr: 0 mismatches" in out.stdout, out.stdout + out.stderr
+
+
+def test_medium_4k_batch_bitexact(disflow_mod, oracle):
+    # BASELINE config 3 (3840x2160 MEDIUM, the LDS/HBM tiling stress case):
+    # a batch of 2 (2-lanes-per-patch kernels on the big levels, 2 streams),
+    # both pairs against the oracle
+    W, H = 3840, 2160
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    pairs = [disflow_mod.synth_pair(900 + k, W, H) for k in range(2)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    got = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2).calc_batch(I0, I1)
+    for k in range(2):
+        _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"4k pair {k}")
+
+
+def test_bench_batch_matches_single_pair_calls(disflow_mod):
+    # the bench configuration (32 x 1080p MEDIUM per call, 2 sub-batch streams,
+    # per-level lane layouts chosen by batch size) gives every pair exactly the
+    # flow of a one-pair call (different lane layouts on some levels)
+    W, H, B = 1920, 1080, 32
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    pairs = [disflow_mod.synth_pair(k, W, H) for k in range(B)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    batch = disflow_mod.DenseInverseSearch(p, W, H, max_batch=B).calc_batch(I0, I1)
+    one = disflow_mod.DenseInverseSearch(p, W, H, max_batch=1)
+    for k in (0, 7, 16, 31):
+        _assert_bitexact(batch[k], one.calc(I0[k], I1[k]), f"pair {k}")
