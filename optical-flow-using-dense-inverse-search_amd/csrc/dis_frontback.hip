@@ -34,7 +34,7 @@ constexpr int kPyrT = DIS_PYR_THREADS;  // threads per pyramid workgroup
 template <int LEVELS>
 __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
 {
-    constexpr int T0 = 1 << LEVELS, SS = T0 + 2, NLOAD = (SS * SS + kPyrT - 1) / kPyrT;
+    constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
     constexpr int N1 = T0 / 2;
     __shared__ uint8_t srcs[2][SS * SS];
     __shared__ float bufs0[2][N1 * N1];
@@ -98,7 +98,6 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     for (int f = 0; f < 2; ++f) {
     const uint8_t* src = srcs[f];
     float* buf0 = bufs0[f];
-    float* buf1 = bufs1[f];
     float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
     // level 1 (and level 0 when requested). A work item is a 2x2 block of
     // level-1 pixels = a 4x4 block of level-0 magnitudes read from a 6x6 u8
@@ -159,28 +158,29 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
             }
     }
 
-    // levels 2..LEVELS from LDS, ping-pong buf0 <-> buf1
-    float* cur = buf0;
-    float* nxt = buf1;
+    }
+
+    // levels 2..LEVELS from LDS for both frames at once (one barrier per
+    // level), ping-pong bufs0 <-> bufs1
 #pragma unroll
     for (int l = 2; l <= LEVELS; ++l) {
         __syncthreads();
-        const int ns = T0 >> (l - 1), nd = ns / 2;
-        float* const pl = planes + a.off[l] + (size_t)(ty >> l) * a.w[l] + (tx >> l);
-        for (int k = tid; k < nd * nd; k += kPyrT) {
-            const int y = k / nd, x = k - y * nd;
+        const int ns = T0 >> (l - 1), nd = ns / 2, nn = nd * nd;
+        for (int k = tid; k < 2 * nn; k += kPyrT) {
+            const int f = k >= nn, kk = k - f * nn;
+            const float* cur = (l & 1) ? bufs1[f] : bufs0[f];
+            float* nxt = (l & 1) ? bufs0[f] : bufs1[f];
+            float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+            float* const pl = planes + a.off[l] + (size_t)(ty >> l) * a.w[l] + (tx >> l);
+            const int y = kk / nd, x = kk - y * nd;
             const float* p = cur + (2 * y) * ns + 2 * x;
             float s = p[0] + p[1];
             s = s + p[ns];
             s = s + p[ns + 1];
             const float v = s * 0.25f;
-            nxt[k] = v;
+            nxt[kk] = v;
             pl[y * a.w[l] + x] = v;
         }
-        float* t = cur;
-        cur = nxt;
-        nxt = t;
-    }
     }
 }
 

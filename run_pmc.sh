@@ -13,7 +13,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float)); n = colle
 for r in csv.DictReader(open(sys.argv[1])):
     k = (r['Kernel_Name'][:26], int(r['Grid_Size']))
     agg[k][r['Counter_Name']] += float(r['Counter_Value']); n[k].add(r['Dispatch_Id'])
-for k, c in sorted(agg.items(), key=lambda kv: -kv[1]['SQ_INSTS_VALU'])[:3]:
+for k, c in sorted(agg.items(), key=lambda kv: -kv[1]['SQ_INSTS_VALU'])[:int(__import__('os').environ.get('TOPK', '3'))]:
     m = len(n[k]); w = c['SQ_WAVES'] / m
     d = {x: v / m for x, v in c.items()}
     print(k, ' '.join(f"{x}={v:.4g}" for x, v in d.items()))
