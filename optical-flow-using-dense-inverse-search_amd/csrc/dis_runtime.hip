@@ -463,19 +463,22 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         if (st == DIS_OK) c->last_batch = n;
         return st;
     }
+    // sub-batch 0 runs on the caller's stream itself (no cross-queue hop
+    // between consecutive calls); 1..S-1 fork from it and join back into it
     DIS_HIP(hipEventRecord(c->fork, s));
     const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
     for (int k = 0; k < S; ++k) {
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
-        DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+        hipStream_t sk = k == 0 ? s : c->sub[k];
+        if (k > 0) DIS_HIP(hipStreamWaitEvent(sk, c->fork, 0));
         dis_status st = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride, stride,
-                                  pair_stride, flow + (size_t)a * fpp, c->sub[k],
+                                  pair_stride, flow + (size_t)a * fpp, sk,
                                   (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
                                   DIS_STAGGER ? c->staged[k] : nullptr);
         if (st != DIS_OK) return st;
-        DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
+        if (k > 0) DIS_HIP(hipEventRecord(c->join[k], sk));
     }
-    for (int k = 0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
+    for (int k = 1; k < S; ++k) DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     c->last_batch = n;
     return DIS_OK;
 }
