@@ -115,6 +115,27 @@ private:
     int width_, height_;
 };
 
+// Middlebury colour coding (src/color_coding.cpp draw_optical_flow) of n
+// W x H (u,v) fields into BGR u8, on the GPU.
+inline void flow_color(const float* flow, int n, int width, int height, uint8_t* bgr, float maxmotion = -1.0f,
+                       dis_mem where = DIS_MEM_HOST, void* stream = nullptr, int device = 0)
+{
+    check(dis_flow_color(flow, n, width, height, maxmotion, bgr, where, stream, device));
+}
+
+// Middlebury .flo files (src/IO_flow.cpp ReadFlowFile / SaveFlowFile).
+inline void write_flo(const std::string& path, const float* data, int width, int height, int channels = 2)
+{
+    check(dis_write_flo(path.c_str(), data, width, height, channels));
+}
+inline std::vector<float> read_flo(const std::string& path, int* width, int* height, int channels = 2)
+{
+    check(dis_flo_info(path.c_str(), width, height));
+    std::vector<float> v((size_t)*width * *height * channels);
+    check(dis_read_flo(path.c_str(), v.data(), *width, *height, channels));
+    return v;
+}
+
 }  // namespace dis
 
 namespace OpticalFlow {

@@ -165,6 +165,25 @@ dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* d
 dis_status dis_set_kernel_timing(dis_ctx* ctx, int enable);
 dis_status dis_kernel_time(dis_ctx* ctx, int kernel, int* launches, double* total_ms);
 
+/* Middlebury flow colour coding, src/color_coding.cpp:13-117 (draw_optical_flow
+ * with compute_color): n W x H (u,v) float fields (interleaved, row-major,
+ * pair stride W*H*2) to n W x H x 3 u8 BGR images (OpenCV Vec3b order).
+ * maxmotion > 0 fixes the motion range; <= 0 uses max(1, max |u| over valid
+ * pixels) per field, as the reference's default -1. Invalid vectors (NaN or
+ * |component| >= 1e9) are black. Host pointers: synchronous; device pointers:
+ * asynchronous on `stream`. Runs on HIP device `device`. */
+dis_status dis_flow_color(const float* flow, int n, int width, int height, float maxmotion, uint8_t* bgr,
+                          dis_mem where, void* stream, int device);
+
+/* Middlebury .flo files (src/IO_flow.cpp:10-98): "PIEH", int32 width,
+ * int32 height, width*height*channels float32 row-major interleaved,
+ * little-endian; channels 1 (depth), 2 (flow) or 4 (scene flow). Host only
+ * (no GPU). Reading validates the tag, the size against the buffer and the
+ * exact file length. */
+dis_status dis_flo_info(const char* path, int* width, int* height);
+dis_status dis_read_flo(const char* path, float* data, int width, int height, int channels);
+dis_status dis_write_flo(const char* path, const float* data, int width, int height, int channels);
+
 /* Deterministic synthetic pair (SURVEY.md 8d generator): multi-octave value
  * noise I0 and I1 = I0 warped by a smooth sinusoidal flow; optional
  * ground-truth flow (W*H*2). Host memory, host compute; seed k -> pair k. */

@@ -121,4 +121,9 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 
+// Middlebury colour coding of n W x H (u,v) fields into BGR u8 (dis_color.hip);
+// maxbits: n device uints of scratch.
+hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmotion, uint8_t* bgr,
+                             unsigned int* maxbits, hipStream_t s);
+
 }  // namespace dis

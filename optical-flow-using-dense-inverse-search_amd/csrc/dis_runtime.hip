@@ -35,6 +35,9 @@ dis_status fail(dis_status s, const std::string& msg)
 
 namespace dis {
 
+// error reporting for the host-only translation units (dis_io.cpp)
+dis_status set_error(dis_status s, const std::string& msg) { return fail(s, msg); }
+
 bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 {
     std::memset(g, 0, sizeof(*g));
@@ -931,6 +934,46 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
     }
     hipStreamSynchronize(s);
     cleanup();
+    return rc;
+}
+
+dis_status dis_flow_color(const float* flow, int n, int width, int height, float maxmotion, uint8_t* bgr,
+                          dis_mem where, void* stream, int device)
+{
+    if (!flow || !bgr) return fail(DIS_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n < 1 || width < 1 || height < 1) return fail(DIS_ERR_INVALID_ARGUMENT, "n, width, height must be >= 1");
+    if (where != DIS_MEM_HOST && where != DIS_MEM_DEVICE) return fail(DIS_ERR_INVALID_ARGUMENT, "bad dis_mem");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(DIS_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(DIS_ERR_INVALID_ARGUMENT, "device index out of range");
+    DIS_HIP(hipSetDevice(device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t fbytes = sizeof(float) * 2 * (size_t)width * height * n;
+    const size_t cbytes = (size_t)3 * width * height * n;
+    if (where == DIS_MEM_DEVICE) {
+        unsigned int* maxbits = nullptr;
+        DIS_HIP(hipMallocAsync(reinterpret_cast<void**>(&maxbits), sizeof(unsigned int) * n, s));
+        const hipError_t e = dis::launch_flow_color(flow, n, width, height, maxmotion, bgr, maxbits, s);
+        DIS_HIP(hipFreeAsync(maxbits, s));
+        DIS_HIP(e);
+        return DIS_OK;
+    }
+    float* dflow = nullptr;
+    uint8_t* dbgr = nullptr;
+    unsigned int* maxbits = nullptr;
+    dis_status rc = DIS_OK;
+    if (hipMalloc(&dflow, fbytes) != hipSuccess || hipMalloc(&dbgr, cbytes) != hipSuccess ||
+        hipMalloc(&maxbits, sizeof(unsigned int) * n) != hipSuccess) {
+        rc = fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
+    } else if (hipMemcpyAsync(dflow, flow, fbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+               dis::launch_flow_color(dflow, n, width, height, maxmotion, dbgr, maxbits, s) != hipSuccess ||
+               hipMemcpyAsync(bgr, dbgr, cbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipStreamSynchronize(s) != hipSuccess) {
+        rc = fail(DIS_ERR_DEVICE, "flow colour coding failed");
+    }
+    hipFree(dflow);
+    hipFree(dbgr);
+    hipFree(maxbits);
     return rc;
 }
 

@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "dis_workload_info", "dis_create", "dis_destroy", "dis_calc_u8", "dis_calc_batch_u8",
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
-    "dis_set_concurrency",
+    "dis_set_concurrency", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
 )
 
 
@@ -149,6 +149,10 @@ def lib() -> ctypes.CDLL:
         L.dis_set_kernel_timing.argtypes = [V, I]
         L.dis_kernel_time.argtypes = [V, I, P(I), P(D)]
         L.dis_synth_pair.argtypes = [ctypes.c_uint64, I, I, V, V, V]
+        L.dis_flow_color.argtypes = [V, I, I, I, ctypes.c_float, V, I, V, I]
+        L.dis_flo_info.argtypes = [ctypes.c_char_p, P(I), P(I)]
+        L.dis_read_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
+        L.dis_write_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
         for name in EXPORTED_SYMBOLS:
             if name not in ("dis_abi_version", "dis_last_error"):
                 getattr(L, name).restype = I
@@ -179,6 +183,38 @@ def workload(params: Params, width: int, height: int) -> dict:
     w = _Workload()
     _check(lib().dis_workload_info(ctypes.byref(params._c()), width, height, ctypes.byref(w)))
     return {k: getattr(w, k) for k, _ in _Workload._fields_}
+
+
+def flow_color(flow: np.ndarray, maxmotion: float = -1.0, device: int = 0) -> np.ndarray:
+    """Middlebury colour coding (src/color_coding.cpp draw_optical_flow) of an
+    (H, W, 2) or (n, H, W, 2) float field on the GPU -> u8 BGR (..., 3)."""
+    f = np.ascontiguousarray(flow, dtype=np.float32)
+    single = f.ndim == 3
+    if single:
+        f = f[None]
+    if f.ndim != 4 or f.shape[-1] != 2:
+        raise DisError(DIS_ERR_INVALID_ARGUMENT, "flow must be (H, W, 2) or (n, H, W, 2)")
+    n, H, W = f.shape[:3]
+    out = np.empty((n, H, W, 3), np.uint8)
+    _check(lib().dis_flow_color(_ptr(f), n, W, H, float(maxmotion), _ptr(out), MEM_HOST, None, device))
+    return out[0] if single else out
+
+
+def read_flo(path: str, channels: int = 2) -> np.ndarray:
+    """Read a Middlebury .flo file (src/IO_flow.cpp:10-53) -> (H, W, channels) float32."""
+    w, h = ctypes.c_int(), ctypes.c_int()
+    _check(lib().dis_flo_info(os.fsencode(path), ctypes.byref(w), ctypes.byref(h)))
+    out = np.empty((h.value, w.value, channels), np.float32)
+    _check(lib().dis_read_flo(os.fsencode(path), _ptr(out), w.value, h.value, channels))
+    return out
+
+
+def write_flo(path: str, data: np.ndarray) -> None:
+    """Write (H, W, channels) float32 as a .flo file (src/IO_flow.cpp:56-98)."""
+    d = np.ascontiguousarray(data, dtype=np.float32)
+    if d.ndim == 2:
+        d = d[..., None]
+    _check(lib().dis_write_flo(os.fsencode(path), _ptr(d), d.shape[1], d.shape[0], d.shape[2]))
 
 
 def synth_pair(seed: int, width: int, height: int, with_gt: bool = False):

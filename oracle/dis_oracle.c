@@ -614,3 +614,68 @@ int dis_oracle_calc_u8(const dis_oracle_params* p, int W, int H,
     free(flowF); free(f0); free(f1); free(img0); free(dx0); free(dy0); free(img1);
     return rc;
 }
+
+/* ---- colour coding (src/color_coding.cpp) ---------------- */
+
+/* is_flow_correct, src/color_coding.cpp:8-11 */
+static int flow_ok(float x, float y)
+{
+    return !(x != x) && !(y != y) && fabsf(x) < 1e9f && fabsf(y) < 1e9f;
+}
+
+/* compute_color, src/color_coding.cpp:13-79: colour wheel (:31-56, integer
+ * division), angle, linear interpolation between wheel entries, saturation
+ * by radius, BGR store with truncation (:76). */
+static void compute_color(float fx, float fy, uint8_t* pix)
+{
+    enum { RY = 15, YG = 6, GC = 4, CB = 11, BM = 13, MR = 6, NCOLS = RY + YG + GC + CB + BM + MR };
+    int wheel[NCOLS][3];
+    int k = 0, i, b;
+    for (i = 0; i < RY; ++i, ++k) { wheel[k][0] = 255; wheel[k][1] = 255 * i / RY; wheel[k][2] = 0; }
+    for (i = 0; i < YG; ++i, ++k) { wheel[k][0] = 255 - 255 * i / YG; wheel[k][1] = 255; wheel[k][2] = 0; }
+    for (i = 0; i < GC; ++i, ++k) { wheel[k][0] = 0; wheel[k][1] = 255; wheel[k][2] = 255 * i / GC; }
+    for (i = 0; i < CB; ++i, ++k) { wheel[k][0] = 0; wheel[k][1] = 255 - 255 * i / CB; wheel[k][2] = 255; }
+    for (i = 0; i < BM; ++i, ++k) { wheel[k][0] = 255 * i / BM; wheel[k][1] = 0; wheel[k][2] = 255; }
+    for (i = 0; i < MR; ++i, ++k) { wheel[k][0] = 255; wheel[k][1] = 0; wheel[k][2] = 255 - 255 * i / MR; }
+    {
+        const float rad = sqrtf(fx * fx + fy * fy);
+        const float a = (float)atan2(-(double)fy, -(double)fx) / 3.14159274f; /* / (float)CV_PI */
+        const float fk = (a + 1.0f) / 2.0f * (float)(NCOLS - 1);
+        const int k0 = (int)fk;
+        const int k1 = (k0 + 1) % NCOLS;
+        const float f = fk - (float)k0;
+        for (b = 0; b < 3; b++) {
+            const float col0 = (float)wheel[k0][b] / 255.f;
+            const float col1 = (float)wheel[k1][b] / 255.f;
+            float col = (1 - f) * col0 + f * col1;
+            if (rad <= 1)
+                col = 1 - rad * (1 - col);
+            else
+                col *= .75f;
+            pix[2 - b] = (uint8_t)(255.f * col);
+        }
+    }
+}
+
+/* draw_optical_flow, src/color_coding.cpp:81-117 */
+void dis_oracle_flow_color(const float* flow, int W, int H, float maxmotion, uint8_t* bgr)
+{
+    float maxrad = maxmotion;
+    long long i, n = (long long)W * H;
+    memset(bgr, 0, (size_t)n * 3);
+    if (maxmotion <= 0) {
+        maxrad = 1;
+        for (i = 0; i < n; ++i) {
+            const float x = flow[2 * i], y = flow[2 * i + 1];
+            if (!flow_ok(x, y)) continue;
+            {
+                const float r = sqrtf(x * x + y * y);
+                maxrad = maxrad > r ? maxrad : r;
+            }
+        }
+    }
+    for (i = 0; i < n; ++i) {
+        const float x = flow[2 * i], y = flow[2 * i + 1];
+        if (flow_ok(x, y)) compute_color(x / maxrad, y / maxrad, bgr + 3 * i);
+    }
+}

@@ -38,6 +38,7 @@ def _load():
     L.dis_oracle_pad_convert.argtypes = [V, Z, I, I, I, V]
     L.dis_oracle_pyramid.argtypes = [V, I, I, I, V, V, V]
     L.dis_oracle_sobel.argtypes = [V, I, I, V, V]
+    L.dis_oracle_flow_color.argtypes = [V, I, I, F, V]
     L.dis_oracle_flow_from_pyramids.argtypes = [P(V)] * 4 + [I, V, I, I, I, I, I, I, F, I, V, V]
     L.dis_oracle_flow_from_pyramids.restype = I
     L.dis_oracle_upsample_crop.argtypes = [V, I, I, I, I, I, I, I, V]
@@ -183,3 +184,12 @@ def build_pyramids(I0, I1, C, ps):
     PY = pad_planes([p[2] for p in py0], ps, "constant")
     P1 = pad_planes([p[0] for p in py1], ps, "edge")
     return f0.shape[1], f0.shape[0], P0, PX, PY, P1, py0, py1
+
+
+def flow_color(flow, maxmotion=-1.0):
+    """Middlebury colour coding of one (H, W, 2) field -> (H, W, 3) u8 BGR."""
+    f = np.ascontiguousarray(flow, dtype=np.float32)
+    H, W = f.shape[:2]
+    out = np.empty((H, W, 3), np.uint8)
+    lib.dis_oracle_flow_color(f.ctypes.data, W, H, float(maxmotion), out.ctypes.data)
+    return out

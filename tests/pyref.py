@@ -177,3 +177,49 @@ def densify(us, geom, W, H, ps, st):
     m = w > 0
     f[m] = f[m] / w[m][:, None]
     return f
+
+
+def flow_color(flow, maxmotion=-1.0):
+    """Vectorised float32 restatement of draw_optical_flow / compute_color
+    (src/color_coding.cpp:13-117), independent of the C oracle."""
+    f32 = np.float32
+    wheel = []
+    for i in range(15):
+        wheel.append((255, 255 * i // 15, 0))
+    for i in range(6):
+        wheel.append((255 - 255 * i // 6, 255, 0))
+    for i in range(4):
+        wheel.append((0, 255, 255 * i // 4))
+    for i in range(11):
+        wheel.append((0, 255 - 255 * i // 11, 255))
+    for i in range(13):
+        wheel.append((255 * i // 13, 0, 255))
+    for i in range(6):
+        wheel.append((255, 0, 255 - 255 * i // 6))
+    wheel = np.array(wheel, np.int64)
+    ncols = len(wheel)
+    x = flow[..., 0].astype(f32)
+    y = flow[..., 1].astype(f32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        ok = ~np.isnan(x) & ~np.isnan(y) & (np.abs(x) < f32(1e9)) & (np.abs(y) < f32(1e9))
+        if maxmotion <= 0:
+            r = np.sqrt(x[ok] * x[ok] + y[ok] * y[ok])
+            maxrad = max(f32(1), r.max() if r.size else f32(1))
+        else:
+            maxrad = f32(maxmotion)
+        fx = np.where(ok, x, f32(0)) / f32(maxrad)
+        fy = np.where(ok, y, f32(0)) / f32(maxrad)
+        rad = np.sqrt(fx * fx + fy * fy)
+        a = np.arctan2(-fy.astype(np.float64), -fx.astype(np.float64)).astype(f32) / f32(3.14159274)
+        fk = (a + f32(1)) / f32(2) * f32(ncols - 1)
+        k0 = fk.astype(np.int64)
+        k1 = (k0 + 1) % ncols
+        fr = fk - k0.astype(f32)
+        out = np.zeros(flow.shape[:-1] + (3,), np.uint8)
+        for b in range(3):
+            c0 = wheel[k0, b].astype(f32) / f32(255)
+            c1 = wheel[k1, b].astype(f32) / f32(255)
+            col = (f32(1) - fr) * c0 + fr * c1
+            col = np.where(rad <= f32(1), f32(1) - rad * (f32(1) - col), col * f32(0.75))
+            out[..., 2 - b] = np.where(ok, (f32(255) * col).astype(np.int64), 0).astype(np.uint8)
+    return out

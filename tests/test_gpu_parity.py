@@ -273,3 +273,35 @@ def test_bench_batch_matches_single_pair_calls(disflow_mod):
     one = disflow_mod.DenseInverseSearch(p, W, H, max_batch=1)
     for k in (0, 7, 16, 31):
         _assert_bitexact(batch[k], one.calc(I0[k], I1[k]), f"pair {k}")
+
+
+@pytest.mark.parametrize("maxmotion", [-1.0, 3.0])
+def test_flow_color_kernel_bitexact(disflow_mod, oracle, maxmotion):
+    # dis_flow_color (k_color_maxrad + k_color_pixels) vs the C oracle, byte
+    # for byte: special values, a batch of fields, and an engine flow
+    rng = np.random.default_rng(9)
+    f = (rng.standard_normal((3, 61, 77, 2)) * 5).astype(np.float32)
+    f[0, 0, :6] = [(np.nan, 1), (1, np.inf), (2e9, 0), (0, 0), (-0.0, 0.0), (1e-30, -1e-30)]
+    W, H = 320, 240
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    I0, I1 = disflow_mod.synth_pair(3, W, H)
+    flow = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+    got = disflow_mod.flow_color(f, maxmotion)
+    for k in range(3):
+        assert np.array_equal(got[k], oracle.flow_color(f[k], maxmotion)), f"field {k}"
+    assert np.array_equal(disflow_mod.flow_color(flow, maxmotion), oracle.flow_color(flow, maxmotion))
+
+
+def test_flow_color_device_pointers(disflow_mod, oracle):
+    import torch
+    rng = np.random.default_rng(10)
+    f = (rng.standard_normal((2, 50, 40, 2)) * 3).astype(np.float32)
+    d = torch.from_numpy(f).cuda()
+    out = torch.empty((2, 50, 40, 3), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    disflow_mod._check(disflow_mod.lib().dis_flow_color(d.data_ptr(), 2, 40, 50, -1.0, out.data_ptr(),
+                                                        disflow_mod.MEM_DEVICE, s.cuda_stream, 0))
+    s.synchronize()
+    o = out.cpu().numpy()
+    for k in range(2):
+        assert np.array_equal(o[k], oracle.flow_color(f[k]))

@@ -220,3 +220,35 @@ def test_pad_convert_matches_numpy(oracle):
     got = oracle.pad_convert(img, 3)
     exp = np.pad(img, ((0, 1), (2, 3)), mode="edge").astype(np.float32)  # 152 x 208
     assert got.shape == (152, 208) and np.array_equal(got, exp)
+
+
+def _color_cases():
+    rng = np.random.default_rng(5)
+    f = (rng.standard_normal((37, 53, 2)) * 4).astype(np.float32)
+    f[0, 0] = (np.nan, 1)
+    f[0, 1] = (1, np.inf)
+    f[0, 2] = (2e9, 0)
+    f[0, 3] = (0, 0)
+    f[0, 4] = (-0.0, 0.0)
+    f[1, :8] = [(1, 0), (0, 1), (-1, 0), (0, -1), (3, 4), (-3, 4), (1e-30, 0), (-7, -7)]
+    return f
+
+
+@pytest.mark.parametrize("maxmotion", [-1.0, 0.0, 2.5, 100.0])
+def test_flow_color_oracle_matches_numpy(oracle, maxmotion):
+    f = _color_cases()
+    assert np.array_equal(oracle.flow_color(f, maxmotion), pyref.flow_color(f, maxmotion))
+
+
+def test_flow_color_known_answers(oracle):
+    # src/color_coding.cpp: zero motion is white, invalid is black, the unit
+    # vector +x maps to wheel[0] (red) at full saturation, +y to wheel 13/14
+    f = np.zeros((1, 4, 2), np.float32)
+    f[0, 1] = (1, 0)
+    f[0, 2] = (0, 1)
+    f[0, 3] = (np.nan, 0)
+    c = oracle.flow_color(f, 1.0)
+    assert c[0, 0].tolist() == [255, 255, 255]
+    assert c[0, 1].tolist() == [0, 0, 255]
+    assert c[0, 2].tolist() == [0, 229, 255]
+    assert c[0, 3].tolist() == [0, 0, 0]
