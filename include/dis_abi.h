@@ -61,7 +61,8 @@ typedef struct dis_params {
     int iterations;          /* >= 0; each patch does iterations+1 updates (Q3)          */
     float patch_overlap;     /* [0,1); steps = max(1, floor(ps*(1-overlap))) in float    */
     int patch_normalization; /* 0/1: mean-normalise the warped patch (src/patch.cpp:264) */
-    int var_refine_iters;    /* must be 0: the reference skips refinement (README.md:11) */
+    int var_refine_iters;    /* 0 = the reference (no refinement, README.md:11); > 0: fixed-point iterations of
+                                variational refinement per level (parity unpinned) */
 } dis_params;
 
 typedef struct dis_ctx dis_ctx;

@@ -57,6 +57,8 @@ struct Search8Args {
     int iters, norm;
     int tile_stride;          // LDS tile row stride (search8_tile_stride(steps))
     int lanes_per_patch;      // 1, 2, 4 or 8 (k_search8<LPP>)
+    const float2* dense_coarse;  // non-null: init from the coarser level's DENSE flow (variational
+    long long dense_stride;      //   refinement on) instead of u_coarse; float2 per pair
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline
@@ -125,5 +127,20 @@ hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 // maxbits: n device uints of scratch.
 hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmotion, uint8_t* bgr,
                              unsigned int* maxbits, hipStream_t s);
+
+// Variational refinement of one level's dense flow (dis_varref.hip).
+constexpr int kVarRefPlanes = 21;  // per-pair workspace planes
+constexpr int kVarRefSor = 5;      // red-black SOR sweeps per fixed-point iteration
+struct VarRefArgs {
+    const float* img0;      // level planes of pair 0 (pre-offset), pair stride plane_stride
+    const float* img1;
+    long long plane_stride;
+    float2* flow;           // dense flow of pair 0 (pre-offset), refined in place
+    long long flow_stride;  // float2 per pair
+    float* ws;              // workspace of pair 0, pair stride ws_stride floats
+    long long ws_plane, ws_stride;
+    int W, H, iters;
+};
+hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s);
 
 }  // namespace dis

@@ -143,6 +143,8 @@ struct dis_ctx {
     float* dy = nullptr;
     float2* pu = nullptr;
     float2* dense = nullptr;
+    float* vr_ws = nullptr;  // variational refinement workspace (kVarRefPlanes planes per pair)
+    long long vr_plane = 0;
     // patch-search fallback lists (dis_search8.hip k_search8_fb): per sub-batch
     // k, kMaxLevels counts at fb + k * kMaxLevels, then per (k, level) a list
     // of up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
@@ -181,8 +183,8 @@ dis_status check_params(const dis_params* p, int W, int H)
     if (p->coarsest_scale >= dis::kMaxLevels - 1)
         return fail(DIS_ERR_INVALID_ARGUMENT, "coarsest_scale too large");
     if (p->iterations < 0) return fail(DIS_ERR_INVALID_ARGUMENT, "iterations must be >= 0");
-    if (p->var_refine_iters != 0)
-        return fail(DIS_ERR_UNSUPPORTED, "variational refinement is not implemented (the reference skips it)");
+    if (p->var_refine_iters < 0 || p->var_refine_iters > 64)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "var_refine_iters must be in [0, 64]");
     const int sf = 1 << p->coarsest_scale;
     const int Wp = W + ((W % sf) ? sf - W % sf : 0), Hp = H + ((H % sf) ? sf - H % sf : 0);
     if ((Wp >> p->coarsest_scale) < 1 || (Hp >> p->coarsest_scale) < 1)
@@ -200,6 +202,8 @@ void free_ws(dis_ctx* c)
     hipFree(c->dense);
     hipFree(c->fb);
     c->fb = nullptr;
+    hipFree(c->vr_ws);
+    c->vr_ws = nullptr;
     hipFree(c->in0);
     hipFree(c->in1);
     hipFree(c->out);
@@ -262,6 +266,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     float2* const pu = c->pu + (size_t)p0 * g.u_stride;
     float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant != 1;
+    const bool vr = c->p.var_refine_iters > 0;
     if (wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
     {
         if (fast && g.C >= 1) {
@@ -356,13 +361,17 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
             b.fb_count = fb_count + l;
             b.fb_list = c->fb + c->fb_list_off[sub][l];
+            if (vr && l < g.C) {  // refined dense flows: init from the coarser level's dense field
+                b.dense_coarse = dense + g.lv[l + 1].dense_off;
+                b.dense_stride = g.dense_stride;
+            }
             b.iters = g.iters;
             b.norm = g.norm;
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         }
-        if (fast && !c->debug) continue;  // the fused output kernel densifies the finest level itself
+        if (fast && !c->debug && !vr) continue;  // the fused output kernel densifies the finest level itself
         dis::DensifyArgs d{};
         d.u = pu + L.u_off;
         d.dense = dense + L.dense_off;
@@ -377,6 +386,21 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         d.offw = L.offw;
         d.offh = L.offh;
         DIS_HIP(dis::launch_densify(d, n, s));
+        if (vr) {  // variational refinement of the level's dense flow
+            dis::VarRefArgs v{};
+            v.img0 = img0 + L.plane_off;
+            v.img1 = img1 + L.plane_off;
+            v.plane_stride = g.plane_stride;
+            v.flow = dense + L.dense_off;
+            v.flow_stride = g.dense_stride;
+            v.ws = c->vr_ws + (size_t)p0 * dis::kVarRefPlanes * c->vr_plane;
+            v.ws_plane = c->vr_plane;
+            v.ws_stride = dis::kVarRefPlanes * c->vr_plane;
+            v.W = L.W;
+            v.H = L.H;
+            v.iters = c->p.var_refine_iters;
+            DIS_HIP(dis::launch_var_refine(v, n, s));
+        }
     }
     dis::OutputArgs o{};
     bool fused_out = false;
@@ -401,12 +425,12 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         o.hp = g.ps / 2;
         o.vec_store = ((reinterpret_cast<uintptr_t>(flow) & 15) == 0 && (g.W & 1) == 0) ? 1 : 0;
         o.sc = std::pow(2.0f, (float)g.F);
-        fused_out = dis::output_fits(o);
+        fused_out = dis::output_fits(o) && !vr;  // refined: the finest dense field exists
     }
     if (fused_out) {
         DIS_HIP(dis::launch_output(o, n, s, timing(c, 3)));
     } else {
-        if (fast && !c->debug) {  // the search loop skipped the finest densify: do it here
+        if (fast && !c->debug && !vr) {  // the search loop skipped the finest densify: do it here
             const dis::LevelGeom& L = g.lv[g.F];
             dis::DensifyArgs d{};
             d.u = pu + L.u_off;
@@ -509,7 +533,8 @@ dis_status dis_preset_params(dis_preset preset, int width, int height, dis_param
         case DIS_PRESET_ULTRAFAST: p.patch_overlap = 0.5f; p.iterations = 12; p.finest_scale = 2; break;
         case DIS_PRESET_FAST: p.patch_overlap = 0.5f; p.iterations = 16; p.finest_scale = 2; break;
         case DIS_PRESET_MEDIUM: p.patch_overlap = 0.625f; p.iterations = 25; p.finest_scale = 1; break;
-        case DIS_PRESET_SLOW: p.patch_overlap = 0.75f; p.iterations = 128; p.finest_scale = 0; break;
+        case DIS_PRESET_SLOW:  // + variational refinement (BASELINE config 5; not in the reference)
+            p.patch_overlap = 0.75f; p.iterations = 128; p.finest_scale = 0; p.var_refine_iters = 3; break;
         case DIS_PRESET_REFERENCE:
             // CLI defaults, src/main.cpp:66-71
             p.patch_overlap = 0.7f; p.iterations = 1000; p.finest_scale = 0; p.coarsest_scale = 3;
@@ -626,6 +651,10 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
             }
         ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
              hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess;
+    }
+    if (ok && params->var_refine_iters > 0) {
+        c->vr_plane = (long long)g.lv[g.F].W * g.lv[g.F].H;  // the largest refined level
+        ok = hipMalloc(&c->vr_ws, sizeof(float) * dis::kVarRefPlanes * c->vr_plane * B) == hipSuccess;
     }
     // pipelined sub-batches: later sub-batches get the higher priority, so the
     // workgroups of their latency-bound coarse levels are dispatched as soon

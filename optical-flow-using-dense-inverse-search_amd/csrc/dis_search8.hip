@@ -392,7 +392,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int hp = 4;
     int ga = 0, ha = 0, PH = 0, PN = 0;
     float2 cuv[kCuPer<LPP>];
-    const float2* uc = a.u_coarse ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
+    const float2* uc = (a.u_coarse && !a.dense_coarse) ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
     if (uc) {
         const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
         const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
@@ -513,7 +513,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2,
     // gathered from the staged coarse displacements.
     float ix = 0.0f, iy = 0.0f;
-    if (uc && active) {
+    if (a.dense_coarse && active) {
+        // from the coarser level's dense flow (refined): src/patch_grid.cpp:108-119
+        const float2 d = a.dense_coarse[(size_t)pair * a.dense_stride + (size_t)(iry >> 1) * (W / 2) + (irx >> 1)];
+        ix = d.x * 2;
+        iy = d.y * 2;
+    } else if (uc && active) {
         const int2 xr = crng[gx - bgx0], yr = crng[BX + gy - bgy0];
         float fx = 0.0f, fy = 0.0f, wt = 0.0f;
         for (int cx = xr.x; cx <= xr.y; ++cx)

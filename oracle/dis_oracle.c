@@ -393,6 +393,219 @@ static void densify(const level_ctx* c, int npw, int nph, int steps, int offw, i
 }
 
 /* ------------------------------------------------------------------------- */
+/* variational refinement (absent from the reference,        */
+/* README.md:11 -- PARITY UNPINNED by construction). The DIS paper's          */
+/* refinement as OpenCV's VariationalRefinement structures it (Kroeger et al.  */
+/* 2016, Sec. 2.3; Brox et al. 2004): minimise                                 */
+/*   E = delta*Psi(I_z^2) + gamma*Psi(|grad I_z|^2) + alpha*Psi(|grad u|^2 + |grad v|^2), */
+/* Psi(s^2) = sqrt(s^2 + eps^2), linearised around the current flow, lagged    */
+/* nonlinearity: each of `fp` iterations re-warps I1 by the current flow,      */
+/* linearises, solves for the increment with SOR_ITERS red-black SOR sweeps    */
+/* and adds it. Every expression and its order below is the spec the HIP       */
+/* kernels (dis_varref.hip) follow bit for bit.                                */
+/* ------------------------------------------------------------------------- */
+
+#ifndef VR_ALPHA
+#define VR_ALPHA 20.0f
+#endif
+#ifndef VR_GAMMA
+#define VR_GAMMA 10.0f
+#endif
+#ifndef VR_DELTA
+#define VR_DELTA 5.0f
+#endif
+#define VR_ZETA 0.1f
+#define VR_EPS2 1e-6f /* eps = 0.001 */
+#define VR_OMEGA 1.6f
+#define VR_SOR_ITERS 5
+
+static int clampi_(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* replicate border */
+static float vr_at(const float* f, int stride, int W, int H, int x, int y)
+{
+    return f[(size_t)clampi_(y, 0, H - 1) * stride + clampi_(x, 0, W - 1)];
+}
+
+/* 5-tap derivative (1, -8, 0, 8, -1) / 12 along (dx, dy), replicate border */
+static float vr_d(const float* f, int stride, int W, int H, int x, int y, int dx, int dy)
+{
+    const float a = vr_at(f, stride, W, H, x - 2 * dx, y - 2 * dy), b = vr_at(f, stride, W, H, x - dx, y - dy);
+    const float c = vr_at(f, stride, W, H, x + dx, y + dy), d = vr_at(f, stride, W, H, x + 2 * dx, y + 2 * dy);
+    return (((a - 8.0f * b) + 8.0f * c) - d) / 12.0f;
+}
+
+/* I1 sampled at (x + u, y + v): bilinear, replicate border. The position is
+ * first clamped to [-1, W] x [-1, H] (no effect on the value: beyond it both
+ * taps clamp to the same edge pixel; keeps the float->int conversion defined). */
+static float vr_warp(const float* I1, int stride, int W, int H, float X, float Y)
+{
+    X = fminf(fmaxf(X, -1.0f), (float)W);
+    Y = fminf(fmaxf(Y, -1.0f), (float)H);
+    const float fx0 = floorf(X), fy0 = floorf(Y);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = X - fx0, fy = Y - fy0;
+    const float a = vr_at(I1, stride, W, H, x0, y0), b = vr_at(I1, stride, W, H, x0 + 1, y0);
+    const float c = vr_at(I1, stride, W, H, x0, y0 + 1), d = vr_at(I1, stride, W, H, x0 + 1, y0 + 1);
+    const float top = (1.0f - fx) * a + fx * b;
+    const float bot = (1.0f - fx) * c + fx * d;
+    return (1.0f - fy) * top + fy * bot;
+}
+
+/* flow: dense W*H*2 (u,v interleaved), refined in place. I0/I1 row stride `stride`. */
+void dis_oracle_var_refine(const float* I0, const float* I1, int stride, int W, int H, float* flow, int fp)
+{
+    const size_t n = (size_t)W * H;
+    float* P = (float*)calloc(n * 21, sizeof(float));
+    float *I1w = P, *I0x = P + n, *I0y = P + 2 * n, *Wx = P + 3 * n, *Wy = P + 4 * n;
+    float *Ix = P + 5 * n, *Iy = P + 6 * n, *Iz = P + 7 * n, *Ixx = P + 8 * n, *Ixy = P + 9 * n, *Iyy = P + 10 * n;
+    float *Ixz = P + 11 * n, *Iyz = P + 12 * n, *du = P + 13 * n, *dv = P + 14 * n, *sw = P + 15 * n;
+    float *A11 = P + 16 * n, *A12 = P + 17 * n, *A22 = P + 18 * n, *B1 = P + 19 * n, *B2 = P + 20 * n;
+    int x, y, it, k, color;
+    for (y = 0; y < H; ++y)
+        for (x = 0; x < W; ++x) {
+            const size_t i = (size_t)y * W + x;
+            I0x[i] = vr_d(I0, stride, W, H, x, y, 1, 0);
+            I0y[i] = vr_d(I0, stride, W, H, x, y, 0, 1);
+        }
+    for (it = 0; it < fp; ++it) {
+        /* 1. warp I1 by the current flow; derivatives of the pair */
+        for (y = 0; y < H; ++y)
+            for (x = 0; x < W; ++x) {
+                const size_t i = (size_t)y * W + x;
+                I1w[i] = vr_warp(I1, stride, W, H, (float)x + flow[2 * i], (float)y + flow[2 * i + 1]);
+            }
+        for (y = 0; y < H; ++y)
+            for (x = 0; x < W; ++x) {
+                const size_t i = (size_t)y * W + x;
+                Wx[i] = vr_d(I1w, W, W, H, x, y, 1, 0);
+                Wy[i] = vr_d(I1w, W, W, H, x, y, 0, 1);
+            }
+        for (y = 0; y < H; ++y)
+            for (x = 0; x < W; ++x) {
+                const size_t i = (size_t)y * W + x;
+                Ix[i] = 0.5f * (Wx[i] + I0x[i]);
+                Iy[i] = 0.5f * (Wy[i] + I0y[i]);
+                Iz[i] = I1w[i] - vr_at(I0, stride, W, H, x, y);
+                Ixx[i] = 0.5f * (vr_d(Wx, W, W, H, x, y, 1, 0) + vr_d(I0x, W, W, H, x, y, 1, 0));
+                Ixy[i] = 0.5f * (vr_d(Wx, W, W, H, x, y, 0, 1) + vr_d(I0x, W, W, H, x, y, 0, 1));
+                Iyy[i] = 0.5f * (vr_d(Wy, W, W, H, x, y, 0, 1) + vr_d(I0y, W, W, H, x, y, 0, 1));
+                Ixz[i] = Wx[i] - I0x[i];
+                Iyz[i] = Wy[i] - I0y[i];
+            }
+        /* 2. smoothness weight per pixel, alpha * Psi'(|grad u|^2 + |grad v|^2),
+         * forward differences (0 at the last column / row) */
+        for (y = 0; y < H; ++y)
+            for (x = 0; x < W; ++x) {
+                const size_t i = (size_t)y * W + x;
+                const float uc = flow[2 * i], vc = flow[2 * i + 1];
+                float gxu = 0.0f, gxv = 0.0f, gyu = 0.0f, gyv = 0.0f;
+                if (x < W - 1) {
+                    gxu = flow[2 * (i + 1)] - uc;
+                    gxv = flow[2 * (i + 1) + 1] - vc;
+                }
+                if (y < H - 1) {
+                    gyu = flow[2 * (i + W)] - uc;
+                    gyv = flow[2 * (i + W) + 1] - vc;
+                }
+                sw[i] = VR_ALPHA / sqrtf((((gxu * gxu + gyu * gyu) + gxv * gxv) + gyv * gyv) + VR_EPS2);
+            }
+        /* 3. data weights at the current flow (du = dv = 0: Psi' of the residuals)
+         * and the normal equations of the linearised energy in (du, dv) */
+        for (y = 0; y < H; ++y)
+            for (x = 0; x < W; ++x) {
+                const size_t i = (size_t)y * W + x;
+                const float psiI = VR_DELTA / sqrtf(Iz[i] * Iz[i] + VR_EPS2);
+                const float psiG = VR_GAMMA / sqrtf((Ixz[i] * Ixz[i] + Iyz[i] * Iyz[i]) + VR_EPS2);
+                A11[i] = (psiI * (Ix[i] * Ix[i]) + psiG * (Ixx[i] * Ixx[i] + Ixy[i] * Ixy[i])) + VR_ZETA;
+                A12[i] = psiI * (Ix[i] * Iy[i]) + psiG * (Ixx[i] * Ixy[i] + Ixy[i] * Iyy[i]);
+                A22[i] = (psiI * (Iy[i] * Iy[i]) + psiG * (Ixy[i] * Ixy[i] + Iyy[i] * Iyy[i])) + VR_ZETA;
+                {
+                    const float wl = x > 0 ? sw[i - 1] : 0.0f, wr = x < W - 1 ? sw[i] : 0.0f;
+                    const float wu = y > 0 ? sw[i - W] : 0.0f, wd = y < H - 1 ? sw[i] : 0.0f;
+                    const size_t il = x > 0 ? i - 1 : i, ir = x < W - 1 ? i + 1 : i;
+                    const size_t iu = y > 0 ? i - W : i, id = y < H - 1 ? i + W : i;
+                    const float u = flow[2 * i], v = flow[2 * i + 1];
+                    const float su = ((wl * (flow[2 * il] - u) + wr * (flow[2 * ir] - u)) + wu * (flow[2 * iu] - u)) +
+                                     wd * (flow[2 * id] - u);
+                    const float sv = ((wl * (flow[2 * il + 1] - v) + wr * (flow[2 * ir + 1] - v)) +
+                                      wu * (flow[2 * iu + 1] - v)) +
+                                     wd * (flow[2 * id + 1] - v);
+                    B1[i] = su - (psiI * (Iz[i] * Ix[i]) + psiG * (Ixz[i] * Ixx[i] + Iyz[i] * Ixy[i]));
+                    B2[i] = sv - (psiI * (Iz[i] * Iy[i]) + psiG * (Ixz[i] * Ixy[i] + Iyz[i] * Iyy[i]));
+                }
+                du[i] = 0.0f;
+                dv[i] = 0.0f;
+            }
+        /* 4. red-black SOR on (du, dv): colour 0 = (x + y) even first */
+        for (k = 0; k < VR_SOR_ITERS; ++k)
+            for (color = 0; color < 2; ++color)
+                for (y = 0; y < H; ++y)
+                    for (x = (y + color) & 1; x < W; x += 2) {
+                        const size_t i = (size_t)y * W + x;
+                        const float wl = x > 0 ? sw[i - 1] : 0.0f, wr = x < W - 1 ? sw[i] : 0.0f;
+                        const float wu = y > 0 ? sw[i - W] : 0.0f, wd = y < H - 1 ? sw[i] : 0.0f;
+                        const size_t il = x > 0 ? i - 1 : i, ir = x < W - 1 ? i + 1 : i;
+                        const size_t iu = y > 0 ? i - W : i, id = y < H - 1 ? i + W : i;
+                        const float sumw = ((wl + wr) + wu) + wd;
+                        const float sdu = ((wl * du[il] + wr * du[ir]) + wu * du[iu]) + wd * du[id];
+                        const float nu = (1.0f - VR_OMEGA) * du[i] +
+                                         VR_OMEGA * (((B1[i] + sdu) - A12[i] * dv[i]) / (A11[i] + sumw));
+                        const float sdv = ((wl * dv[il] + wr * dv[ir]) + wu * dv[iu]) + wd * dv[id];
+                        const float nv = (1.0f - VR_OMEGA) * dv[i] +
+                                         VR_OMEGA * (((B2[i] + sdv) - A12[i] * nu) / (A22[i] + sumw));
+                        du[i] = nu;
+                        dv[i] = nv;
+                    }
+        /* 5. flow += (du, dv) */
+        for (size_t i = 0; i < n; ++i) {
+            flow[2 * i] = flow[2 * i] + du[i];
+            flow[2 * i + 1] = flow[2 * i + 1] + dv[i];
+        }
+    }
+    free(P);
+}
+
+/* the refinement energy of a flow (for the energy-decrease checks):
+ * sum over pixels of delta*Psi(Iz^2) + gamma*Psi(Ixz^2 + Iyz^2) + alpha*Psi(|grad u|^2 + |grad v|^2)
+ * with the warp and derivatives of the flow itself (double accumulation). */
+double dis_oracle_var_energy(const float* I0, const float* I1, int stride, int W, int H, const float* flow)
+{
+    const size_t n = (size_t)W * H;
+    float* P = (float*)calloc(n * 5, sizeof(float));
+    float *I1w = P, *I0x = P + n, *I0y = P + 2 * n, *Wx = P + 3 * n, *Wy = P + 4 * n;
+    double e = 0.0;
+    int x, y;
+    for (y = 0; y < H; ++y)
+        for (x = 0; x < W; ++x) {
+            const size_t i = (size_t)y * W + x;
+            I1w[i] = vr_warp(I1, stride, W, H, (float)x + flow[2 * i], (float)y + flow[2 * i + 1]);
+        }
+    for (y = 0; y < H; ++y)
+        for (x = 0; x < W; ++x) {
+            const size_t i = (size_t)y * W + x;
+            I0x[i] = vr_d(I0, stride, W, H, x, y, 1, 0);
+            I0y[i] = vr_d(I0, stride, W, H, x, y, 0, 1);
+            Wx[i] = vr_d(I1w, W, W, H, x, y, 1, 0);
+            Wy[i] = vr_d(I1w, W, W, H, x, y, 0, 1);
+        }
+    for (y = 0; y < H; ++y)
+        for (x = 0; x < W; ++x) {
+            const size_t i = (size_t)y * W + x;
+            const double iz = (double)I1w[i] - vr_at(I0, stride, W, H, x, y);
+            const double gx = (double)Wx[i] - I0x[i], gy = (double)Wy[i] - I0y[i];
+            const double ux = x < W - 1 ? (double)flow[2 * (i + 1)] - flow[2 * i] : 0.0;
+            const double vx = x < W - 1 ? (double)flow[2 * (i + 1) + 1] - flow[2 * i + 1] : 0.0;
+            const double uy = y < H - 1 ? (double)flow[2 * (i + W)] - flow[2 * i] : 0.0;
+            const double vy = y < H - 1 ? (double)flow[2 * (i + W) + 1] - flow[2 * i + 1] : 0.0;
+            e += VR_DELTA * sqrt(iz * iz + 1e-6) + VR_GAMMA * sqrt(gx * gx + gy * gy + 1e-6) +
+                 VR_ALPHA * sqrt(ux * ux + uy * uy + vx * vx + vy * vy + 1e-6);
+        }
+    free(P);
+    return e;
+}
+
+/* ------------------------------------------------------------------------- */
 /* a15: scale loop (src/optical_flow.cpp:19-91)                                */
 /* ------------------------------------------------------------------------- */
 
@@ -401,6 +614,18 @@ int dis_oracle_flow_from_pyramids(
     float* const* img_second, int img_padding, float* outflow,
     int width, int height, int coarsest, int finest, int iterations,
     int patch_size, float patch_overlap, int patch_normalization,
+    float* dbg_patch_u, float* dbg_dense)
+{
+    return dis_oracle_flow_from_pyramids_vr(img_first, img_first_dx, img_first_dy, img_second, img_padding, outflow,
+                                            width, height, coarsest, finest, iterations, patch_size, patch_overlap,
+                                            patch_normalization, 0, dbg_patch_u, dbg_dense);
+}
+
+int dis_oracle_flow_from_pyramids_vr(
+    float* const* img_first, float* const* img_first_dx, float* const* img_first_dy,
+    float* const* img_second, int img_padding, float* outflow,
+    int width, int height, int coarsest, int finest, int iterations,
+    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters,
     float* dbg_patch_u, float* dbg_dense)
 {
     if (patch_size < 2 || (patch_size & 1) || patch_size * patch_size > 1024) return -1;
@@ -449,9 +674,12 @@ int dis_oracle_flow_from_pyramids(
                              rx, ry, ix, iy, gdx, gdy, second, &pu[2 * ip], &pu[2 * ip + 1]);
             }
         densify(&c, npw, nph, steps, offw, offh, pu, dense);     /* :86-90 */
+        if (var_refine_iters > 0)                                /* SURVEY 8f row 1 (not in the reference) */
+            dis_oracle_var_refine(img_first[scale] + (size_t)img_padding * c.tmp_w + img_padding,
+                                  img_second[scale] + (size_t)img_padding * c.tmp_w + img_padding, c.tmp_w,
+                                  c.width, c.height, dense, var_refine_iters); /* pixel (0,0) of the padded planes */
         flows[scale] = dense;
         pus[scale] = pu;
-        (void)img_first;
     }
     /* debug capture, levels 0..C in order */
     for (int l = 0; l <= coarsest; ++l) {
@@ -606,9 +834,9 @@ int dis_oracle_calc_u8(const dis_oracle_params* p, int W, int H,
         off += (size_t)w * h;
     }
     float* flowF = (float*)malloc(sizeof(float) * 2 * (size_t)(Wp >> F) * (Hp >> F));
-    int rc = dis_oracle_flow_from_pyramids(P0, PX, PY, P1, ps, flowF, Wp, Hp, C, F,
+    int rc = dis_oracle_flow_from_pyramids_vr(P0, PX, PY, P1, ps, flowF, Wp, Hp, C, F,
                                            p->iterations, ps, p->patch_overlap,
-                                           p->patch_normalization, NULL, NULL);
+                                           p->patch_normalization, p->var_refine_iters, NULL, NULL);
     if (rc == 0) dis_oracle_upsample_crop(flowF, Wp, Hp, F, pl, pt, W, H, flow_out);
     for (int l = 0; l <= C; ++l) { free(P0[l]); free(PX[l]); free(PY[l]); free(P1[l]); }
     free(flowF); free(f0); free(f1); free(img0); free(dx0); free(dy0); free(img1);

@@ -31,6 +31,7 @@ typedef struct {
     int iterations;          /* include/optical_flow.hpp:42 */
     float patch_overlap;     /* src/optical_flow.cpp:490 */
     int patch_normalization; /* include/optical_flow.hpp:43 */
+    int var_refine_iters;    /* 0 = the reference (no refinement) */
 } dis_oracle_params;
 
 /* Grid geometry of one level (src/optical_flow.cpp:490, src/patch_grid.cpp:20-23). */
@@ -67,6 +68,22 @@ int dis_oracle_flow_from_pyramids(
     int width, int height, int coarsest, int finest, int iterations,
     int patch_size, float patch_overlap, int patch_normalization,
     float* dbg_patch_u, float* dbg_dense);
+
+/* As above, plus `var_refine_iters` fixed-point iterations of variational
+ * refinement on each level's dense flow after densification (SURVEY 8f row 1;
+ * absent from the reference: parity unpinned). 0 = the reference. */
+int dis_oracle_flow_from_pyramids_vr(
+    float* const* img_first, float* const* img_first_dx, float* const* img_first_dy,
+    float* const* img_second, int img_padding, float* outflow,
+    int width, int height, int coarsest, int finest, int iterations,
+    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters,
+    float* dbg_patch_u, float* dbg_dense);
+
+/* Variational refinement of one level's dense flow (W*H*2, in place) between
+ * level images I0, I1 (row stride `stride`), `fp` fixed-point iterations;
+ * and the energy it decreases. Specification in dis_oracle.c. */
+void dis_oracle_var_refine(const float* I0, const float* I1, int stride, int W, int H, float* flow, int fp);
+double dis_oracle_var_energy(const float* I0, const float* I1, int stride, int W, int H, const float* flow);
 
 /* a16: scale by 2^F, bilinear upsample (OpenCV INTER_LINEAR semantics) and
  * crop the padding (src/main.cpp:191-198). flowF is (Wp>>F)*(Hp>>F)*2. */

@@ -22,6 +22,7 @@ class Params(ctypes.Structure):
         ("iterations", ctypes.c_int),
         ("patch_overlap", ctypes.c_float),
         ("patch_normalization", ctypes.c_int),
+        ("var_refine_iters", ctypes.c_int),
     ]
 
 
@@ -39,6 +40,9 @@ def _load():
     L.dis_oracle_pyramid.argtypes = [V, I, I, I, V, V, V]
     L.dis_oracle_sobel.argtypes = [V, I, I, V, V]
     L.dis_oracle_flow_color.argtypes = [V, I, I, F, V]
+    L.dis_oracle_var_refine.argtypes = [V, V, I, I, I, V, I]
+    L.dis_oracle_var_energy.argtypes = [V, V, I, I, I, V]
+    L.dis_oracle_var_energy.restype = ctypes.c_double
     L.dis_oracle_flow_from_pyramids.argtypes = [P(V)] * 4 + [I, V, I, I, I, I, I, I, F, I, V, V]
     L.dis_oracle_flow_from_pyramids.restype = I
     L.dis_oracle_upsample_crop.argtypes = [V, I, I, I, I, I, I, I, V]
@@ -155,9 +159,9 @@ def upsample_crop(flowF, Wp, Hp, F, pl, pt, W, H):
     return out
 
 
-def calc_u8(I0, I1, C, F, ps, it, overlap, norm=1):
+def calc_u8(I0, I1, C, F, ps, it, overlap, norm=1, vr=0):
     H, W = I0.shape
-    p = Params(C, F, ps, it, overlap, norm)
+    p = Params(C, F, ps, it, overlap, norm, vr)
     out = np.empty((H, W, 2), np.float32)
     a0 = np.ascontiguousarray(I0, dtype=np.uint8)
     a1 = np.ascontiguousarray(I1, dtype=np.uint8)
@@ -169,7 +173,8 @@ def calc_u8(I0, I1, C, F, ps, it, overlap, norm=1):
 def calc_from_params(I0, I1, params):
     """params: disflow.Params (or anything with the same attributes)."""
     return calc_u8(I0, I1, params.coarsest_scale, params.finest_scale, params.patch_size,
-                   params.iterations, params.patch_overlap, params.patch_normalization)
+                   params.iterations, params.patch_overlap, params.patch_normalization,
+                   getattr(params, "var_refine_iters", 0))
 
 
 def build_pyramids(I0, I1, C, ps):
@@ -193,3 +198,21 @@ def flow_color(flow, maxmotion=-1.0):
     out = np.empty((H, W, 3), np.uint8)
     lib.dis_oracle_flow_color(f.ctypes.data, W, H, float(maxmotion), out.ctypes.data)
     return out
+
+
+def var_refine(I0, I1, flow, fp):
+    """Variational refinement of a (H, W, 2) flow between float level images."""
+    a0 = np.ascontiguousarray(I0, dtype=np.float32)
+    a1 = np.ascontiguousarray(I1, dtype=np.float32)
+    f = np.array(flow, dtype=np.float32, copy=True, order="C")
+    H, W = a0.shape
+    lib.dis_oracle_var_refine(_p(a0), _p(a1), W, W, H, _p(f), int(fp))
+    return f
+
+
+def var_energy(I0, I1, flow):
+    a0 = np.ascontiguousarray(I0, dtype=np.float32)
+    a1 = np.ascontiguousarray(I1, dtype=np.float32)
+    f = np.ascontiguousarray(flow, dtype=np.float32)
+    H, W = a0.shape
+    return lib.dis_oracle_var_energy(_p(a0), _p(a1), W, W, H, _p(f))

@@ -60,7 +60,8 @@ def test_presets(disflow_mod):
     ("finest_scale", 7, -1),      # F > C
     ("finest_scale", -1, -1),
     ("iterations", -1, -1),
-    ("var_refine_iters", 3, -2),  # not implemented: UNSUPPORTED
+    ("var_refine_iters", 65, -1),  # refinement iterations in [0, 64]
+    ("var_refine_iters", -1, -1),
 ])
 def test_validation_errors(disflow_mod, field, value, status):
     p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, 1920, 1080)

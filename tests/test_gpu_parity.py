@@ -305,3 +305,33 @@ def test_flow_color_device_pointers(disflow_mod, oracle):
     o = out.cpu().numpy()
     for k in range(2):
         assert np.array_equal(o[k], oracle.flow_color(f[k]))
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_var_refine_path_bitexact(disflow_mod, oracle, variant):
+    # variational refinement on every level (fast search with dense-flow init,
+    # k_vr_* kernels) vs the oracle's restatement, a batch of 3 on 2 streams;
+    # variant 1 = the generic kernels
+    W, H = 320, 240
+    p = disflow_mod.Params(coarsest_scale=4, finest_scale=1, patch_size=8, iterations=10, patch_overlap=0.625,
+                           patch_normalization=1, var_refine_iters=3)
+    pairs = [disflow_mod.synth_pair(60 + k, W, H) for k in range(3)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=3)
+    eng.set_variant(variant)
+    got = eng.calc_batch(I0, I1)
+    for k in range(3):
+        _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"pair {k}")
+
+
+def test_slow_preset_with_refinement_bitexact(disflow_mod, oracle):
+    # BASELINE config 5 semantics (SLOW: F = 0, steps 2, refinement on) at a
+    # small size with fewer search iterations
+    W, H = 192, 144
+    p = disflow_mod.preset_params(disflow_mod.Preset.SLOW, W, H)
+    assert p.var_refine_iters > 0 and p.finest_scale == 0
+    p.iterations = 8
+    I0, I1 = disflow_mod.synth_pair(70, W, H)
+    got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+    _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "slow + refinement")

@@ -252,3 +252,48 @@ def test_flow_color_known_answers(oracle):
     assert c[0, 1].tolist() == [0, 0, 255]
     assert c[0, 2].tolist() == [0, 229, 255]
     assert c[0, 3].tolist() == [0, 0, 0]
+
+
+# ---- variational refinement (not in the reference) ----------
+
+def _vr_case(seed, W=160, H=120):
+    import disflow
+    I0, I1, gt = disflow.synth_pair(seed, W, H, with_gt=True)
+    lv0 = [oracle_binding_levels(I) for I in (I0, I1)]
+    return I0, I1, gt, lv0[0], lv0[1]
+
+
+def oracle_binding_levels(I):
+    import oracle_binding as ob
+    return ob.pyramid(ob.pad_convert(I, 0), 0)[0][0]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_var_refine_decreases_energy(oracle, seed):
+    # energy of the refined DIS flow below that of the unrefined one (the
+    # refinement's purpose), on the level-0 images the path refines on
+    I0, I1, gt, m0, m1 = _vr_case(seed)
+    flow = oracle.calc_u8(I0, I1, 3, 0, 8, 12, 0.5)
+    e0 = oracle.var_energy(m0, m1, flow)
+    for fp in (1, 2, 3):
+        assert oracle.var_energy(m0, m1, oracle.var_refine(m0, m1, flow, fp)) < e0
+
+
+def test_var_refine_zero_iterations_is_identity(oracle):
+    I0, I1, gt, m0, m1 = _vr_case(4)
+    flow = oracle.calc_u8(I0, I1, 3, 0, 8, 12, 0.5)
+    assert np.array_equal(oracle.var_refine(m0, m1, flow, 0), flow)
+    assert np.array_equal(oracle.calc_u8(I0, I1, 3, 0, 8, 12, 0.5, 1, 0), flow)
+
+
+def test_var_refine_improves_synthetic_accuracy(oracle):
+    # mean end-point error vs the generator's ground truth over seeds, the whole
+    # coarse-to-fine path with refinement on every level (3 fixed-point iterations)
+    import disflow
+    e = {0: [], 3: []}
+    for seed in (3, 4, 5, 6):
+        I0, I1, gt = disflow.synth_pair(seed, 320, 240, with_gt=True)
+        for vr in e:
+            f = oracle.calc_u8(I0, I1, 4, 0, 8, 16, 0.75, 1, vr)
+            e[vr].append(np.sqrt(((f - gt) ** 2).sum(-1)).mean())
+    assert np.mean(e[3]) < 0.85 * np.mean(e[0])
