@@ -124,12 +124,12 @@ hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 
 // Middlebury colour coding of n W x H (u,v) fields into BGR u8 (dis_color.hip);
-// maxbits: n device uints of scratch.
+// maxbits: 32 * n device uints of scratch.
 hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmotion, uint8_t* bgr,
                              unsigned int* maxbits, hipStream_t s);
 
 // Variational refinement of one level's dense flow (dis_varref.hip).
-constexpr int kVarRefPlanes = 21;  // per-pair workspace planes
+constexpr int kVarRefPlanes = 8;   // per-pair workspace planes
 constexpr int kVarRefSor = 5;      // red-black SOR sweeps per fixed-point iteration
 struct VarRefArgs {
     const float* img0;      // level planes of pair 0 (pre-offset), pair stride plane_stride

@@ -136,6 +136,14 @@ struct dis_ctx {
     hipEvent_t fork = nullptr;
     hipEvent_t join[kMaxSub] = {};
     hipEvent_t staged[kMaxSub] = {};  // sub-batch k's pyramid done (pipelined start of k+1)
+    // variational refinement: its ~16 launches per fixed-point iteration per level
+    // are replayed as one HIP graph per (sub-batch, level), captured on first use
+    // (all pointers are context workspace; re-captured when the slice changes)
+    struct VrGraph {
+        hipGraphExec_t exec = nullptr;
+        int n = -1, p0 = -1;
+    } vrg[kMaxSub][dis::kMaxLevels];
+    hipStream_t cap = nullptr;  // capture-only stream
     // workspace (device)
     float* img0 = nullptr;
     float* img1 = nullptr;
@@ -251,9 +259,19 @@ int upsample_xmax(const dis::Geometry& g)
     return g.Wp;
 }
 
-// The whole path for n pairs already resident in device memory.
+#ifndef DIS_VR_GRAPH
+#define DIS_VR_GRAPH 1  // replay each level's refinement launches as a HIP graph
+#endif
+
+constexpr int kStageFront = 1000, kStageBack = -1000;  // other stages: the level index
+
+// One stage of the path for n pairs already resident in device memory: the
+// front end (pyramid), one level (search, and densify + refinement when on),
+// or the back end (output). run_batches issues the stages stage-major across
+// the sub-batches, so every sub-batch's next kernels are queued early even
+// when the host is slow to enqueue a long stage.
 dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
-                     size_t pair_stride, float2* flow, hipStream_t s, hipEvent_t wait_pyr = nullptr,
+                     size_t pair_stride, float2* flow, hipStream_t s, int stage, hipEvent_t wait_pyr = nullptr,
                      hipEvent_t pyr_done = nullptr)
 {
     int* const fb_count = c->fb + (size_t)sub * dis::kMaxLevels;  // this sub-batch's fallback counts
@@ -267,8 +285,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant != 1;
     const bool vr = c->p.var_refine_iters > 0;
-    if (wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
-    {
+    if (stage == kStageFront && wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
+    if (stage == kStageFront) {
         if (fast && g.C >= 1) {
             dis::PyramidArgs pa{};
             pa.I0 = I0;
@@ -304,6 +322,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, img0, gdx, gdy, n, s));
     }
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
+        if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
         dis::SearchArgs a{};
         a.img0 = img0;
@@ -399,9 +418,31 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             v.W = L.W;
             v.H = L.H;
             v.iters = c->p.var_refine_iters;
-            DIS_HIP(dis::launch_var_refine(v, n, s));
+            auto& G = c->vrg[sub][l];
+            if (!DIS_VR_GRAPH) {
+                DIS_HIP(dis::launch_var_refine(v, n, s));
+                continue;
+            }
+            if (G.n != n || G.p0 != p0) {
+                if (G.exec) hipGraphExecDestroy(G.exec);
+                G.exec = nullptr;
+                G.n = G.p0 = -1;
+                hipGraph_t graph = nullptr;
+                DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+                const hipError_t e = dis::launch_var_refine(v, n, c->cap);
+                const hipError_t e2 = hipStreamEndCapture(c->cap, &graph);
+                DIS_HIP(e);
+                DIS_HIP(e2);
+                const hipError_t e3 = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
+                hipGraphDestroy(graph);
+                DIS_HIP(e3);
+                G.n = n;
+                G.p0 = p0;
+            }
+            DIS_HIP(hipGraphLaunch(G.exec, s));
         }
     }
+    if (stage != kStageBack) return DIS_OK;
     dis::OutputArgs o{};
     bool fused_out = false;
     if (fast) {
@@ -470,6 +511,9 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
 #ifndef DIS_STAGGER
 #define DIS_STAGGER 0  // measured: lockstep sub-batches 1-3% faster on 1080p MEDIUM (search dominates)
 #endif
+#ifndef DIS_STAGE_MAJOR
+#define DIS_STAGE_MAJOR 1
+#endif
 #ifndef DIS_STAGGER_PRIO
 #define DIS_STAGGER_PRIO DIS_STAGGER
 #endif
@@ -484,28 +528,42 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
 dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                        size_t pair_stride, float2* flow, hipStream_t s)
 {
-    const int S = std::min(c->nsub, n);
+    // refinement: one stream. Its many short bandwidth-bound kernels stall
+    // behind a co-running sub-batch's long search launches (measured on
+    // 3840x2160 SLOW, batch 2: 36.3 ms with two streams, 24.1 ms with one).
+    const int S = c->p.var_refine_iters > 0 ? 1 : std::min(c->nsub, n);
+    std::vector<int> stages = {kStageFront};
+    for (int l = c->g.C; l >= c->g.F; --l) stages.push_back(l);
+    stages.push_back(kStageBack);
     if (S <= 1) {
-        dis_status st = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s);
-        if (st == DIS_OK) c->last_batch = n;
-        return st;
+        for (int st : stages) {
+            dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
+            if (r != DIS_OK) return r;
+        }
+        c->last_batch = n;
+        return DIS_OK;
     }
     // sub-batch 0 runs on the caller's stream itself (no cross-queue hop
     // between consecutive calls); 1..S-1 fork from it and join back into it
     DIS_HIP(hipEventRecord(c->fork, s));
+    for (int k = 1; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
     const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
-    for (int k = 0; k < S; ++k) {
+    const bool stage_major = DIS_STAGE_MAJOR;
+    for (size_t i = 0; i < stages.size() * S; ++i) {
+        const int k = stage_major ? (int)(i % S) : (int)(i / stages.size());
+        const int st = stage_major ? stages[i / S] : stages[i % stages.size()];
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
         hipStream_t sk = k == 0 ? s : c->sub[k];
-        if (k > 0) DIS_HIP(hipStreamWaitEvent(sk, c->fork, 0));
-        dis_status st = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride, stride,
-                                  pair_stride, flow + (size_t)a * fpp, sk,
-                                  (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
-                                  DIS_STAGGER ? c->staged[k] : nullptr);
-        if (st != DIS_OK) return st;
-        if (k > 0) DIS_HIP(hipEventRecord(c->join[k], sk));
+        dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
+                                 stride, pair_stride, flow + (size_t)a * fpp, sk, st,
+                                 (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
+                                 DIS_STAGGER ? c->staged[k] : nullptr);
+        if (r != DIS_OK) return r;
     }
-    for (int k = 1; k < S; ++k) DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
+    for (int k = 1; k < S; ++k) {
+        DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
+        DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
+    }
     c->last_batch = n;
     return DIS_OK;
 }
@@ -641,6 +699,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->in1, (size_t)width * height * B) == hipSuccess &&
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
     if (ok) {
         size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
@@ -674,6 +733,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
             if (c->staged[k]) hipEventDestroy(c->staged[k]);
         }
         if (c->fork) hipEventDestroy(c->fork);
+        if (c->cap) hipStreamDestroy(c->cap);
         if (c->own) hipStreamDestroy(c->own);
         delete c;
         return fail(DIS_ERR_OUT_OF_MEMORY, "device workspace allocation failed");
@@ -696,6 +756,10 @@ dis_status dis_destroy(dis_ctx* c)
         if (c->staged[k]) hipEventDestroy(c->staged[k]);
     }
     if (c->fork) hipEventDestroy(c->fork);
+    for (auto& row : c->vrg)
+        for (auto& G : row)
+            if (G.exec) hipGraphExecDestroy(G.exec);
+    if (c->cap) hipStreamDestroy(c->cap);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return DIS_OK;
@@ -981,7 +1045,7 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     const size_t cbytes = (size_t)3 * width * height * n;
     if (where == DIS_MEM_DEVICE) {
         unsigned int* maxbits = nullptr;
-        DIS_HIP(hipMallocAsync(reinterpret_cast<void**>(&maxbits), sizeof(unsigned int) * n, s));
+        DIS_HIP(hipMallocAsync(reinterpret_cast<void**>(&maxbits), sizeof(unsigned int) * 32 * n, s));
         const hipError_t e = dis::launch_flow_color(flow, n, width, height, maxmotion, bgr, maxbits, s);
         DIS_HIP(hipFreeAsync(maxbits, s));
         DIS_HIP(e);
@@ -992,7 +1056,7 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     unsigned int* maxbits = nullptr;
     dis_status rc = DIS_OK;
     if (hipMalloc(&dflow, fbytes) != hipSuccess || hipMalloc(&dbgr, cbytes) != hipSuccess ||
-        hipMalloc(&maxbits, sizeof(unsigned int) * n) != hipSuccess) {
+        hipMalloc(&maxbits, sizeof(unsigned int) * 32 * n) != hipSuccess) {
         rc = fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
     } else if (hipMemcpyAsync(dflow, flow, fbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
                dis::launch_flow_color(dflow, n, width, height, maxmotion, dbgr, maxbits, s) != hipSuccess ||

@@ -4,16 +4,23 @@
 // oracle/dis_oracle.c, which is the specification -- same expressions, same
 // order, -ffp-contract=off, so the results are bit-identical).
 //
-// Per fixed-point iteration (re-warp, linearise, red-black SOR):
-//   k_vr_warp   I1w = I1(x + u, y + v)          bilinear, replicate border
-//   k_vr_d1     Wx, Wy = 5-tap derivatives of I1w
-//   k_vr_d2     Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz
-//   k_vr_smooth s = alpha / sqrt(|grad u|^2 + |grad v|^2 + eps^2)
-//   k_vr_data   A11, A12, A22, B1, B2 of the normal equations, du = dv = 0
-//   k_vr_sor<c> x VR_SOR_ITERS x 2 colours (a colour's pixels are independent)
-//   k_vr_apply  flow += (du, dv)
-// (k_vr_d0: I0x, I0y once per level.) Planes are per pair, W_l x H_l floats,
-// in a context workspace; grid = (pixels / 256, pairs).
+// Two launches per fixed-point iteration (re-warp, linearise, red-black SOR):
+//   k_vr_lin  one 64x16 tile of pixels: I1 warped by the current flow over the
+//             tile +-4 (bilinear, replicate border), its 5-tap derivatives over
+//             the tile +-2, the smoothness weights alpha/sqrt(|grad u|^2 +
+//             |grad v|^2 + eps^2) over the tile + its left column / top row --
+//             all staged in LDS -- then per pixel the data weights and the
+//             normal equations: B1, B2, A12, D1 = A11 + sum w, D2 = A22 + sum w
+//             and the pixel's own weight, six planes of the workspace.
+//   k_vr_sor  all VR_SOR sweeps x 2 colours of the red-black SOR on a 108x46
+//             tile, in LDS, on the tile + a halo of 10 columns / 9 rows: du =
+//             dv = 0 everywhere at the first half-sweep, and every later
+//             half-sweep can be wrong only one pixel further in from the
+//             halo's outer edge, so after the 10th the tile itself is exact
+//             (the halo is recomputed by the neighbouring tiles). Then
+//             flow += (du, dv) on the tile.
+// (k_vr_d0: I0x, I0y once per level.) The planes are per pair, W_l x H_l
+// floats, in a context workspace of kVarRefPlanes planes per pair.
 #include <hip/hip_runtime.h>
 
 #include "dis_kernels.h"
@@ -24,10 +31,8 @@ namespace {
 
 constexpr float kAlpha = 20.0f, kGamma = 10.0f, kDelta = 5.0f, kZeta = 0.1f, kEps2 = 1e-6f, kOmega = 1.6f;
 
-enum Plane {
-    P_I1W, P_I0X, P_I0Y, P_WX, P_WY, P_IX, P_IY, P_IZ, P_IXX, P_IXY, P_IYY, P_IXZ, P_IYZ,
-    P_DU, P_DV, P_SW, P_A11, P_A12, P_A22, P_B1, P_B2
-};
+enum Plane { P_I0X, P_I0Y, P_B1, P_B2, P_A12, P_D1, P_D2, P_SW };
+static_assert(P_SW + 1 == kVarRefPlanes, "workspace planes");
 
 struct Lvl {
     const float* img0;  // level planes of pair 0 (pre-offset), pair stride plane_stride
@@ -42,194 +47,271 @@ struct Lvl {
 
 __device__ __forceinline__ int clampi_(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-__device__ __forceinline__ float at(const float* f, int W, int H, int x, int y)
-{
-    return f[(size_t)clampi_(y, 0, H - 1) * W + clampi_(x, 0, W - 1)];
-}
-
-// 5-tap derivative (1, -8, 0, 8, -1) / 12 along (dx, dy), replicate border
-__device__ __forceinline__ float deriv(const float* f, int W, int H, int x, int y, int dx, int dy)
-{
-    const float a = at(f, W, H, x - 2 * dx, y - 2 * dy), b = at(f, W, H, x - dx, y - dy);
-    const float c = at(f, W, H, x + dx, y + dy), d = at(f, W, H, x + 2 * dx, y + 2 * dy);
-    return (((a - 8.0f * b) + 8.0f * c) - d) / 12.0f;
-}
-
-struct Px {
-    int x, y, pair;
-    size_t i;
-    bool ok;
-};
-
-__device__ __forceinline__ Px pixel(const Lvl& L)
-{
-    Px p;
-    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
-    p.pair = blockIdx.y;
-    p.ok = k < (long long)L.W * L.H;
-    p.y = (int)(k / L.W);
-    p.x = (int)(k - (long long)p.y * L.W);
-    p.i = (size_t)k;
-    return p;
-}
-
 __device__ __forceinline__ float* plane(const Lvl& L, int pair, int k)
 {
     return L.ws + (size_t)pair * L.ws_stride + (size_t)k * L.ws_plane;
 }
 
+// 5-tap derivative (1, -8, 0, 8, -1) / 12 of the taps a..d at -2, -1, +1, +2
+__device__ __forceinline__ float d5(float a, float b, float c, float d)
+{
+    return (((a - 8.0f * b) + 8.0f * c) - d) / 12.0f;
+}
+
+// I0x, I0y of the level (replicate border), once per level; 2-D grid
 __global__ void __launch_bounds__(256) k_vr_d0(Lvl L)
 {
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const float* I0 = L.img0 + (size_t)p.pair * L.plane_stride;
-    plane(L, p.pair, P_I0X)[p.i] = deriv(I0, L.W, L.H, p.x, p.y, 1, 0);
-    plane(L, p.pair, P_I0Y)[p.i] = deriv(I0, L.W, L.H, p.x, p.y, 0, 1);
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6), pr = blockIdx.z;
+    if (x >= L.W || y >= L.H) return;
+    const int W = L.W, H = L.H;
+    const float* I0 = L.img0 + (size_t)pr * L.plane_stride;
+    const float* r = I0 + (size_t)y * W;
+    const float gx = d5(r[clampi_(x - 2, 0, W - 1)], r[clampi_(x - 1, 0, W - 1)], r[clampi_(x + 1, 0, W - 1)],
+                        r[clampi_(x + 2, 0, W - 1)]);
+    const float gy = d5(I0[(size_t)clampi_(y - 2, 0, H - 1) * W + x], I0[(size_t)clampi_(y - 1, 0, H - 1) * W + x],
+                        I0[(size_t)clampi_(y + 1, 0, H - 1) * W + x], I0[(size_t)clampi_(y + 2, 0, H - 1) * W + x]);
+    const size_t i = (size_t)y * W + x;
+    plane(L, pr, P_I0X)[i] = gx;
+    plane(L, pr, P_I0Y)[i] = gy;
 }
 
-__global__ void __launch_bounds__(256) k_vr_warp(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const float* I1 = L.img1 + (size_t)p.pair * L.plane_stride;
-    const float2 f = L.flow[(size_t)p.pair * L.flow_stride + p.i];
-    float X = (float)p.x + f.x, Y = (float)p.y + f.y;
-    X = fminf(fmaxf(X, -1.0f), (float)L.W);
-    Y = fminf(fmaxf(Y, -1.0f), (float)L.H);
-    const float fx0 = floorf(X), fy0 = floorf(Y);
-    const int x0 = (int)fx0, y0 = (int)fy0;
-    const float fx = X - fx0, fy = Y - fy0;
-    const float a = at(I1, L.W, L.H, x0, y0), b = at(I1, L.W, L.H, x0 + 1, y0);
-    const float c = at(I1, L.W, L.H, x0, y0 + 1), d = at(I1, L.W, L.H, x0 + 1, y0 + 1);
-    const float top = (1.0f - fx) * a + fx * b;
-    const float bot = (1.0f - fx) * c + fx * d;
-    plane(L, p.pair, P_I1W)[p.i] = (1.0f - fy) * top + fy * bot;
-}
+// ---------------------------------------------------------------------------
+// linearisation
+constexpr int kLW = 64, kLH = 16;             // output tile
+constexpr int kFW = kLW + 8, kFH = kLH + 8;   // flow, warped I1: tile +-4
+constexpr int kGW = kLW + 4, kGH = kLH + 4;   // Wx, Wy, I0x, I0y: tile +-2
+constexpr int kSW = kLW + 1, kSH = kLH + 1;   // smoothness weight: tile + left column, top row
 
-__global__ void __launch_bounds__(256) k_vr_d1(Lvl L)
+// Every staged array is indexed by a logical position relative to the tile;
+// the entry holds the quantity AT THE CLAMPED position, which is what the
+// reference's replicate-border reads of that logical position return. A
+// derivative at logical g is evaluated at c = clamp(g) from the entries at
+// c +- 1, 2 -- each of which again holds the value at the clamped position.
+__global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
 {
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const float* w = plane(L, p.pair, P_I1W);
-    plane(L, p.pair, P_WX)[p.i] = deriv(w, L.W, L.H, p.x, p.y, 1, 0);
-    plane(L, p.pair, P_WY)[p.i] = deriv(w, L.W, L.H, p.x, p.y, 0, 1);
-}
-
-__global__ void __launch_bounds__(256) k_vr_d2(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const int W = L.W, H = L.H, x = p.x, y = p.y;
-    const size_t i = p.i;
-    const float* Wx = plane(L, p.pair, P_WX);
-    const float* Wy = plane(L, p.pair, P_WY);
-    const float* I0x = plane(L, p.pair, P_I0X);
-    const float* I0y = plane(L, p.pair, P_I0Y);
-    const float* I0 = L.img0 + (size_t)p.pair * L.plane_stride;
-    plane(L, p.pair, P_IX)[i] = 0.5f * (Wx[i] + I0x[i]);
-    plane(L, p.pair, P_IY)[i] = 0.5f * (Wy[i] + I0y[i]);
-    plane(L, p.pair, P_IZ)[i] = plane(L, p.pair, P_I1W)[i] - I0[i];
-    plane(L, p.pair, P_IXX)[i] = 0.5f * (deriv(Wx, W, H, x, y, 1, 0) + deriv(I0x, W, H, x, y, 1, 0));
-    plane(L, p.pair, P_IXY)[i] = 0.5f * (deriv(Wx, W, H, x, y, 0, 1) + deriv(I0x, W, H, x, y, 0, 1));
-    plane(L, p.pair, P_IYY)[i] = 0.5f * (deriv(Wy, W, H, x, y, 0, 1) + deriv(I0y, W, H, x, y, 0, 1));
-    plane(L, p.pair, P_IXZ)[i] = Wx[i] - I0x[i];
-    plane(L, p.pair, P_IYZ)[i] = Wy[i] - I0y[i];
-}
-
-__global__ void __launch_bounds__(256) k_vr_smooth(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const int W = L.W;
-    const size_t i = p.i;
-    const float2* f = L.flow + (size_t)p.pair * L.flow_stride;
-    const float uc = f[i].x, vc = f[i].y;
-    float gxu = 0.0f, gxv = 0.0f, gyu = 0.0f, gyv = 0.0f;
-    if (p.x < W - 1) {
-        gxu = f[i + 1].x - uc;
-        gxv = f[i + 1].y - vc;
+    __shared__ float2 sF[kFH][kFW];
+    __shared__ float sI[kFH][kFW];
+    __shared__ float sWx[kGH][kGW], sWy[kGH][kGW], sGx[kGH][kGW], sGy[kGH][kGW];
+    __shared__ float sS[kSH][kSW];
+    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
+    const int x0 = blockIdx.x * kLW, y0 = blockIdx.y * kLH;
+    const float* I0 = L.img0 + (size_t)pr * L.plane_stride;
+    const float* I1 = L.img1 + (size_t)pr * L.plane_stride;
+    const float2* fl = L.flow + (size_t)pr * L.flow_stride;
+    // 1. flow and the warped I1 over the tile +-4
+    for (int k = tid; k < kFW * kFH; k += 256) {
+        const int ly = k / kFW, lx = k - ly * kFW;
+        const int gx = clampi_(x0 - 4 + lx, 0, W - 1), gy = clampi_(y0 - 4 + ly, 0, H - 1);
+        const float2 f = fl[(size_t)gy * W + gx];
+        sF[ly][lx] = f;
+        float X = (float)gx + f.x, Y = (float)gy + f.y;
+        X = fminf(fmaxf(X, -1.0f), (float)W);
+        Y = fminf(fmaxf(Y, -1.0f), (float)H);
+        const float fx0 = floorf(X), fy0 = floorf(Y);
+        const int xa = (int)fx0, ya = (int)fy0;
+        const float fx = X - fx0, fy = Y - fy0;
+        const int c0 = clampi_(xa, 0, W - 1), c1 = clampi_(xa + 1, 0, W - 1);
+        const float* r0 = I1 + (size_t)clampi_(ya, 0, H - 1) * W;
+        const float* r1 = I1 + (size_t)clampi_(ya + 1, 0, H - 1) * W;
+        const float top = (1.0f - fx) * r0[c0] + fx * r0[c1];
+        const float bot = (1.0f - fx) * r1[c0] + fx * r1[c1];
+        sI[ly][lx] = (1.0f - fy) * top + fy * bot;
     }
-    if (p.y < L.H - 1) {
-        gyu = f[i + W].x - uc;
-        gyv = f[i + W].y - vc;
+    // 2. I0x, I0y over the tile +-2
+    for (int k = tid; k < kGW * kGH; k += 256) {
+        const int ly = k / kGW, lx = k - ly * kGW;
+        const size_t i = (size_t)clampi_(y0 - 2 + ly, 0, H - 1) * W + clampi_(x0 - 2 + lx, 0, W - 1);
+        sGx[ly][lx] = plane(L, pr, P_I0X)[i];
+        sGy[ly][lx] = plane(L, pr, P_I0Y)[i];
     }
-    plane(L, p.pair, P_SW)[i] = kAlpha / sqrtf((((gxu * gxu + gyu * gyu) + gxv * gxv) + gyv * gyv) + kEps2);
+    __syncthreads();
+    // 3. Wx, Wy over the tile +-2; smoothness weights (forward differences, 0
+    //    at the last column / row) over the tile + left column / top row
+    for (int k = tid; k < kGW * kGH; k += 256) {
+        const int ly = k / kGW, lx = k - ly * kGW;
+        const int ix = clampi_(x0 - 2 + lx, 0, W - 1) - x0 + 4, iy = clampi_(y0 - 2 + ly, 0, H - 1) - y0 + 4;
+        sWx[ly][lx] = d5(sI[iy][ix - 2], sI[iy][ix - 1], sI[iy][ix + 1], sI[iy][ix + 2]);
+        sWy[ly][lx] = d5(sI[iy - 2][ix], sI[iy - 1][ix], sI[iy + 1][ix], sI[iy + 2][ix]);
+    }
+    for (int k = tid; k < kSW * kSH; k += 256) {
+        const int ly = k / kSW, lx = k - ly * kSW;
+        const int x = x0 - 1 + lx, y = y0 - 1 + ly;
+        if (x < 0 || y < 0 || x >= W || y >= H) continue;  // never read
+        const int fx = lx + 3, fy = ly + 3;
+        const float uc = sF[fy][fx].x, vc = sF[fy][fx].y;
+        float gxu = 0.0f, gxv = 0.0f, gyu = 0.0f, gyv = 0.0f;
+        if (x < W - 1) {
+            gxu = sF[fy][fx + 1].x - uc;
+            gxv = sF[fy][fx + 1].y - vc;
+        }
+        if (y < H - 1) {
+            gyu = sF[fy + 1][fx].x - uc;
+            gyv = sF[fy + 1][fx].y - vc;
+        }
+        sS[ly][lx] = kAlpha / sqrtf((((gxu * gxu + gyu * gyu) + gxv * gxv) + gyv * gyv) + kEps2);
+    }
+    __syncthreads();
+    // 4. per pixel: the data weights at the current flow and the normal
+    //    equations of the linearised energy in (du, dv)
+    for (int k = tid; k < kLW * kLH; k += 256) {
+        const int ly = k / kLW, lx = k - ly * kLW;
+        const int x = x0 + lx, y = y0 + ly;
+        if (x >= W || y >= H) continue;
+        const int gx = lx + 2, gy = ly + 2, fx = lx + 4, fy = ly + 4;
+        const size_t i = (size_t)y * W + x;
+        const float wx = sWx[gy][gx], wy = sWy[gy][gx], i0x = sGx[gy][gx], i0y = sGy[gy][gx];
+        const float Ix = 0.5f * (wx + i0x);
+        const float Iy = 0.5f * (wy + i0y);
+        const float Iz = sI[fy][fx] - I0[i];
+        const float Ixx = 0.5f * (d5(sWx[gy][gx - 2], sWx[gy][gx - 1], sWx[gy][gx + 1], sWx[gy][gx + 2]) +
+                                  d5(sGx[gy][gx - 2], sGx[gy][gx - 1], sGx[gy][gx + 1], sGx[gy][gx + 2]));
+        const float Ixy = 0.5f * (d5(sWx[gy - 2][gx], sWx[gy - 1][gx], sWx[gy + 1][gx], sWx[gy + 2][gx]) +
+                                  d5(sGx[gy - 2][gx], sGx[gy - 1][gx], sGx[gy + 1][gx], sGx[gy + 2][gx]));
+        const float Iyy = 0.5f * (d5(sWy[gy - 2][gx], sWy[gy - 1][gx], sWy[gy + 1][gx], sWy[gy + 2][gx]) +
+                                  d5(sGy[gy - 2][gx], sGy[gy - 1][gx], sGy[gy + 1][gx], sGy[gy + 2][gx]));
+        const float Ixz = wx - i0x;
+        const float Iyz = wy - i0y;
+        const float psiI = kDelta / sqrtf(Iz * Iz + kEps2);
+        const float psiG = kGamma / sqrtf((Ixz * Ixz + Iyz * Iyz) + kEps2);
+        const float A11 = (psiI * (Ix * Ix) + psiG * (Ixx * Ixx + Ixy * Ixy)) + kZeta;
+        const float A12 = psiI * (Ix * Iy) + psiG * (Ixx * Ixy + Ixy * Iyy);
+        const float A22 = (psiI * (Iy * Iy) + psiG * (Ixy * Ixy + Iyy * Iyy)) + kZeta;
+        const float s = sS[ly + 1][lx + 1];
+        const float wl = x > 0 ? sS[ly + 1][lx] : 0.0f, wr = x < W - 1 ? s : 0.0f;
+        const float wu = y > 0 ? sS[ly][lx + 1] : 0.0f, wd = y < H - 1 ? s : 0.0f;
+        const float2 fc = sF[fy][fx];
+        const float2 fl_ = x > 0 ? sF[fy][fx - 1] : fc, fr = x < W - 1 ? sF[fy][fx + 1] : fc;
+        const float2 fu = y > 0 ? sF[fy - 1][fx] : fc, fd = y < H - 1 ? sF[fy + 1][fx] : fc;
+        const float u = fc.x, v = fc.y;
+        const float su = ((wl * (fl_.x - u) + wr * (fr.x - u)) + wu * (fu.x - u)) + wd * (fd.x - u);
+        const float sv = ((wl * (fl_.y - v) + wr * (fr.y - v)) + wu * (fu.y - v)) + wd * (fd.y - v);
+        const float sumw = ((wl + wr) + wu) + wd;
+        plane(L, pr, P_B1)[i] = su - (psiI * (Iz * Ix) + psiG * (Ixz * Ixx + Iyz * Ixy));
+        plane(L, pr, P_B2)[i] = sv - (psiI * (Iz * Iy) + psiG * (Ixz * Ixy + Iyz * Iyy));
+        plane(L, pr, P_A12)[i] = A12;
+        plane(L, pr, P_D1)[i] = A11 + sumw;
+        plane(L, pr, P_D2)[i] = A22 + sumw;
+        plane(L, pr, P_SW)[i] = s;
+    }
 }
 
-struct Nb {
-    float wl, wr, wu, wd;
-    size_t il, ir, iu, id;
+// ---------------------------------------------------------------------------
+// red-black SOR, all sweeps of one fixed-point iteration per tile
+constexpr int kSQ = 64;                  // pixel pairs (even x, odd x) per region row: one wave per row
+constexpr int kSRH = 64;                 // region rows
+constexpr int kSHX = 10, kSHY = 9;       // halo (even in x: pairs start at even x)
+constexpr int kSTW = 2 * kSQ - 2 * kSHX; // 108 output columns
+constexpr int kSTH = kSRH - 2 * kSHY;    // 46 output rows
+constexpr int kSWaves = 16;
+constexpr int kSRows = kSRH / kSWaves;   // region rows per wave
+static_assert(kSHY >= 2 * kVarRefSor - 1 && kSHX >= 2 * kVarRefSor - 1, "SOR halo: one pixel per half-sweep after the first");
+
+// one pixel's equation: the SOR update reads its 4 neighbours of the other
+// colour; at the image border the neighbour is the pixel itself (weight 0)
+struct SorPx {
+    float b1, b2, a12, d1, d2, wl, wr, wu, wd, du, dv;
+    unsigned nb;  // bit 0: x > 0, 1: x < W-1, 2: y > 0, 3: y < H-1, 4: in image
 };
 
-__device__ __forceinline__ Nb neighbours(const float* sw, const Px& p, int W, int H)
+__global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
 {
-    const size_t i = p.i;
-    Nb n;
-    n.wl = p.x > 0 ? sw[i - 1] : 0.0f;
-    n.wr = p.x < W - 1 ? sw[i] : 0.0f;
-    n.wu = p.y > 0 ? sw[i - W] : 0.0f;
-    n.wd = p.y < H - 1 ? sw[i] : 0.0f;
-    n.il = p.x > 0 ? i - 1 : i;
-    n.ir = p.x < W - 1 ? i + 1 : i;
-    n.iu = p.y > 0 ? i - W : i;
-    n.id = p.y < H - 1 ? i + W : i;
-    return n;
-}
-
-__global__ void __launch_bounds__(256) k_vr_data(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    const size_t i = p.i;
-    const int pr = p.pair;
-    const float Ix = plane(L, pr, P_IX)[i], Iy = plane(L, pr, P_IY)[i], Iz = plane(L, pr, P_IZ)[i];
-    const float Ixx = plane(L, pr, P_IXX)[i], Ixy = plane(L, pr, P_IXY)[i], Iyy = plane(L, pr, P_IYY)[i];
-    const float Ixz = plane(L, pr, P_IXZ)[i], Iyz = plane(L, pr, P_IYZ)[i];
-    const float psiI = kDelta / sqrtf(Iz * Iz + kEps2);
-    const float psiG = kGamma / sqrtf((Ixz * Ixz + Iyz * Iyz) + kEps2);
-    plane(L, pr, P_A11)[i] = (psiI * (Ix * Ix) + psiG * (Ixx * Ixx + Ixy * Ixy)) + kZeta;
-    plane(L, pr, P_A12)[i] = psiI * (Ix * Iy) + psiG * (Ixx * Ixy + Ixy * Iyy);
-    plane(L, pr, P_A22)[i] = (psiI * (Iy * Iy) + psiG * (Ixy * Ixy + Iyy * Iyy)) + kZeta;
-    const Nb n = neighbours(plane(L, pr, P_SW), p, L.W, L.H);
-    const float2* f = L.flow + (size_t)pr * L.flow_stride;
-    const float u = f[i].x, v = f[i].y;
-    const float su = ((n.wl * (f[n.il].x - u) + n.wr * (f[n.ir].x - u)) + n.wu * (f[n.iu].x - u)) + n.wd * (f[n.id].x - u);
-    const float sv = ((n.wl * (f[n.il].y - v) + n.wr * (f[n.ir].y - v)) + n.wu * (f[n.iu].y - v)) + n.wd * (f[n.id].y - v);
-    plane(L, pr, P_B1)[i] = su - (psiI * (Iz * Ix) + psiG * (Ixz * Ixx + Iyz * Ixy));
-    plane(L, pr, P_B2)[i] = sv - (psiI * (Iz * Iy) + psiG * (Ixz * Ixy + Iyz * Iyy));
-    plane(L, pr, P_DU)[i] = 0.0f;
-    plane(L, pr, P_DV)[i] = 0.0f;
-}
-
-// one colour of a red-black SOR sweep: pixels with (x + y) & 1 == COLOR
-template <int COLOR>
-__global__ void __launch_bounds__(256) k_vr_sor(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok || ((p.x + p.y) & 1) != COLOR) return;
-    const size_t i = p.i;
-    const int pr = p.pair;
-    float* du = plane(L, pr, P_DU);
-    float* dv = plane(L, pr, P_DV);
-    const Nb n = neighbours(plane(L, pr, P_SW), p, L.W, L.H);
-    const float A11 = plane(L, pr, P_A11)[i], A12 = plane(L, pr, P_A12)[i], A22 = plane(L, pr, P_A22)[i];
-    const float B1 = plane(L, pr, P_B1)[i], B2 = plane(L, pr, P_B2)[i];
-    const float sumw = ((n.wl + n.wr) + n.wu) + n.wd;
-    const float sdu = ((n.wl * du[n.il] + n.wr * du[n.ir]) + n.wu * du[n.iu]) + n.wd * du[n.id];
-    const float nu = (1.0f - kOmega) * du[i] + kOmega * (((B1 + sdu) - A12 * dv[i]) / (A11 + sumw));
-    const float sdv = ((n.wl * dv[n.il] + n.wr * dv[n.ir]) + n.wu * dv[n.iu]) + n.wd * dv[n.id];
-    const float nv = (1.0f - kOmega) * dv[i] + kOmega * (((B2 + sdv) - A12 * nu) / (A22 + sumw));
-    du[i] = nu;
-    dv[i] = nv;
-}
-
-__global__ void __launch_bounds__(256) k_vr_apply(Lvl L)
-{
-    const Px p = pixel(L);
-    if (!p.ok) return;
-    float2* f = L.flow + (size_t)p.pair * L.flow_stride;
-    const float2 v = f[p.i];
-    f[p.i] = make_float2(v.x + plane(L, p.pair, P_DU)[p.i], v.y + plane(L, p.pair, P_DV)[p.i]);
+    // [column parity][region row + 1][pair + 1]; border cells stay 0
+    __shared__ float sU[2][kSRH + 2][kSQ + 2], sV[2][kSRH + 2][kSQ + 2];
+    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
+    const int q = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = blockIdx.x * kSTW, y0 = blockIdx.y * kSTH;
+    const int xs = x0 - kSHX, ys = y0 - kSHY;  // xs even
+    for (int k = tid; k < 2 * (kSRH + 2) * (kSQ + 2); k += 1024) {
+        (&sU[0][0][0])[k] = 0.0f;
+        (&sV[0][0][0])[k] = 0.0f;
+    }
+    SorPx P[kSRows][2];
+    const float* B1 = plane(L, pr, P_B1);
+    const float* B2 = plane(L, pr, P_B2);
+    const float* A12 = plane(L, pr, P_A12);
+    const float* D1 = plane(L, pr, P_D1);
+    const float* D2 = plane(L, pr, P_D2);
+    const float* SW = plane(L, pr, P_SW);
+#pragma unroll
+    for (int j = 0; j < kSRows; ++j) {
+        const int y = ys + wv + kSWaves * j;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            SorPx& p = P[j][c];
+            const int x = xs + 2 * q + c;
+            const bool in = x >= 0 && x < W && y >= 0 && y < H;
+            p.nb = in ? (16u | (x > 0 ? 1u : 0u) | (x < W - 1 ? 2u : 0u) | (y > 0 ? 4u : 0u) | (y < H - 1 ? 8u : 0u)) : 0u;
+            p.b1 = p.b2 = p.a12 = 0.0f;
+            p.d1 = p.d2 = 1.0f;
+            p.wl = p.wr = p.wu = p.wd = 0.0f;
+            p.du = p.dv = 0.0f;
+            if (in) {
+                const size_t i = (size_t)y * W + x;
+                p.b1 = B1[i];
+                p.b2 = B2[i];
+                p.a12 = A12[i];
+                p.d1 = D1[i];
+                p.d2 = D2[i];
+                const float s = SW[i];
+                p.wl = x > 0 ? SW[i - 1] : 0.0f;
+                p.wr = x < W - 1 ? s : 0.0f;
+                p.wu = y > 0 ? SW[i - W] : 0.0f;
+                p.wd = y < H - 1 ? s : 0.0f;
+            }
+        }
+    }
+    __syncthreads();
+    for (int sweep = 0; sweep < kVarRefSor; ++sweep) {
+#pragma unroll
+        for (int colour = 0; colour < 2; ++colour) {
+#pragma unroll
+            for (int j = 0; j < kSRows; ++j) {
+                const int r = wv + kSWaves * j;  // region row
+                const int y = ys + r;
+                // the pixel of this colour in the pair: x parity = c, (x + y) & 1 == colour
+                const int cpar = (colour ^ y) & 1;  // wave-uniform
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (c != cpar) continue;
+                    SorPx& p = P[j][c];
+                    if (!(p.nb & 16u)) continue;
+                    // neighbours (other parity): same row left / right, rows above / below same parity
+                    const int o = 1 - c;
+                    const int ql = c == 0 ? q : q + 1, qr = c == 0 ? q + 1 : q + 2;
+                    const float ul = (p.nb & 1u) ? sU[o][r + 1][ql] : p.du, ur = (p.nb & 2u) ? sU[o][r + 1][qr] : p.du;
+                    const float uu = (p.nb & 4u) ? sU[c][r][q + 1] : p.du, ud = (p.nb & 8u) ? sU[c][r + 2][q + 1] : p.du;
+                    const float vl = (p.nb & 1u) ? sV[o][r + 1][ql] : p.dv, vr = (p.nb & 2u) ? sV[o][r + 1][qr] : p.dv;
+                    const float vu = (p.nb & 4u) ? sV[c][r][q + 1] : p.dv, vd = (p.nb & 8u) ? sV[c][r + 2][q + 1] : p.dv;
+                    const float sdu = ((p.wl * ul + p.wr * ur) + p.wu * uu) + p.wd * ud;
+                    const float nu = (1.0f - kOmega) * p.du + kOmega * (((p.b1 + sdu) - p.a12 * p.dv) / p.d1);
+                    const float sdv = ((p.wl * vl + p.wr * vr) + p.wu * vu) + p.wd * vd;
+                    const float nv = (1.0f - kOmega) * p.dv + kOmega * (((p.b2 + sdv) - p.a12 * nu) / p.d2);
+                    p.du = nu;
+                    p.dv = nv;
+                    sU[c][r + 1][q + 1] = nu;
+                    sV[c][r + 1][q + 1] = nv;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // flow += (du, dv) on the tile
+    float2* fl = L.flow + (size_t)pr * L.flow_stride;
+#pragma unroll
+    for (int j = 0; j < kSRows; ++j) {
+        const int r = wv + kSWaves * j;
+        if (r < kSHY || r >= kSHY + kSTH) continue;
+        const int y = ys + r;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int lx = 2 * q + c - kSHX;
+            const SorPx& p = P[j][c];
+            if (lx < 0 || lx >= kSTW || !(p.nb & 16u)) continue;
+            float2* f = fl + (size_t)y * W + (xs + 2 * q + c);
+            const float2 v = *f;
+            *f = make_float2(v.x + p.du, v.y + p.dv);
+        }
+    }
 }
 
 }  // namespace
@@ -248,20 +330,15 @@ hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s)
     L.ws_stride = a.ws_stride;
     L.W = a.W;
     L.H = a.H;
-    if ((long long)a.W * a.H > a.ws_plane || a.ws_stride < kVarRefPlanes * a.ws_plane) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)(((long long)a.W * a.H + 255) / 256), n), block(256);
-    hipLaunchKernelGGL(k_vr_d0, grid, block, 0, s, L);
+    if (a.W <= 0 || a.H <= 0 || (long long)a.W * a.H > a.ws_plane || a.ws_stride < kVarRefPlanes * a.ws_plane)
+        return hipErrorInvalidValue;
+    const unsigned nn = (unsigned)n;
+    hipLaunchKernelGGL(k_vr_d0, dim3((a.W + 63) / 64, (a.H + 3) / 4, nn), dim3(256), 0, s, L);
+    const dim3 glin((a.W + kLW - 1) / kLW, (a.H + kLH - 1) / kLH, nn);
+    const dim3 gsor((a.W + kSTW - 1) / kSTW, (a.H + kSTH - 1) / kSTH, nn);
     for (int it = 0; it < a.iters; ++it) {
-        hipLaunchKernelGGL(k_vr_warp, grid, block, 0, s, L);
-        hipLaunchKernelGGL(k_vr_d1, grid, block, 0, s, L);
-        hipLaunchKernelGGL(k_vr_d2, grid, block, 0, s, L);
-        hipLaunchKernelGGL(k_vr_smooth, grid, block, 0, s, L);
-        hipLaunchKernelGGL(k_vr_data, grid, block, 0, s, L);
-        for (int k = 0; k < kVarRefSor; ++k) {
-            hipLaunchKernelGGL(k_vr_sor<0>, grid, block, 0, s, L);
-            hipLaunchKernelGGL(k_vr_sor<1>, grid, block, 0, s, L);
-        }
-        hipLaunchKernelGGL(k_vr_apply, grid, block, 0, s, L);
+        hipLaunchKernelGGL(k_vr_lin, glin, dim3(256), 0, s, L);
+        hipLaunchKernelGGL(k_vr_sor, gsor, dim3(1024), 0, s, L);
     }
     return hipGetLastError();
 }

@@ -851,6 +851,31 @@ static int flow_ok(float x, float y)
     return !(x != x) && !(y != y) && fabsf(x) < 1e9f && fabsf(y) < 1e9f;
 }
 
+/* atan2f (src/color_coding.cpp:52) restated as a fixed float algorithm (the
+ * product kernel evaluates the identical one): t = min/max in [0, 1],
+ * atan(t) = t + t z P(z), z = t^2, with the minimax coefficients of ARM's
+ * optimized-routines atanf (<= 3 ulp), then the octant fix-up. */
+static float atan2_dis(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float t = mx > 0.0f ? mn / mx : 0.0f;
+    const float z = t * t;
+    float p = 0x1.01fd88p-8f;
+    float r;
+    p = p * z + -0x1.4c3c60p-6f;
+    p = p * z + 0x1.93a2c0p-5f;
+    p = p * z + -0x1.491f0ep-4f;
+    p = p * z + 0x1.bd7368p-4f;
+    p = p * z + -0x1.24051ep-3f;
+    p = p * z + 0x1.99935ep-3f;
+    p = p * z + -0x1.55555p-2f;
+    r = t + (t * z) * p;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.0f || (x == 0.0f && signbit(x))) r = 3.14159274f - r;
+    return signbit(y) ? -r : r;
+}
+
 /* compute_color, src/color_coding.cpp:13-79: colour wheel (:31-56, integer
  * division), angle, linear interpolation between wheel entries, saturation
  * by radius, BGR store with truncation (:76). */
@@ -867,7 +892,7 @@ static void compute_color(float fx, float fy, uint8_t* pix)
     for (i = 0; i < MR; ++i, ++k) { wheel[k][0] = 255; wheel[k][1] = 0; wheel[k][2] = 255 - 255 * i / MR; }
     {
         const float rad = sqrtf(fx * fx + fy * fy);
-        const float a = (float)atan2(-(double)fy, -(double)fx) / 3.14159274f; /* / (float)CV_PI */
+        const float a = atan2_dis(-fy, -fx) / 3.14159274f; /* / (float)CV_PI */
         const float fk = (a + 1.0f) / 2.0f * (float)(NCOLS - 1);
         const int k0 = (int)fk;
         const int k1 = (k0 + 1) % NCOLS;

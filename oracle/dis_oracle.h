@@ -100,8 +100,8 @@ int dis_oracle_calc_u8(const dis_oracle_params* p, int W, int H,
 /* Middlebury colour coding, draw_optical_flow with
  * compute_color (src/color_coding.cpp:13-117) for one W*H (u,v) field into
  * W*H*3 u8 BGR (OpenCV Vec3b order). maxmotion <= 0: maxrad = max(1, max
- * radius over valid pixels) (:88-104). atan2f (:52) is taken as the double
- * atan2 rounded to float (the product kernel does the same). */
+ * radius over valid pixels) (:88-104). atan2f (:52) is restated as a fixed
+ * float polynomial (the product kernel evaluates the identical one). */
 void dis_oracle_flow_color(const float* flow, int W, int H, float maxmotion, uint8_t* bgr);
 
 #ifdef __cplusplus

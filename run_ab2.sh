@@ -1,6 +1,7 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python tools/ab.py "$@" --rounds 10 2>&1 | tail -6
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/ab_prof -o run -- python3 $GRAFT_REPO_ROOT/tools/ab.py "$@" --rounds 2 > /dev/null 2>&1
-cut -c1-120 $GRAFT_REPO_ROOT/gpurun_out/ab_prof/run_kernel_stats.csv
+L=optical-flow-using-dense-inverse-search_amd/disflow
+timeout -k 10 400 python3 tools/ab.py --spawn 3 --rounds 4 $L/libdis_hip.so $L/libdis_hip_sm.so > gpurun_out/ab_c2.log 2>&1 || { tail gpurun_out/ab_c2.log; exit 1; }
+cat gpurun_out/ab_c2.log | grep -v amdgpu.ids
+timeout -k 10 400 python3 tools/ab.py --spawn 2 --rounds 3 --steps 3 --batch 2 --preset slow --width 3840 --height 2160 $L/libdis_hip.so $L/libdis_hip_sm.so > gpurun_out/ab_c5.log 2>&1 || { tail gpurun_out/ab_c5.log; exit 1; }
+cat gpurun_out/ab_c5.log | grep -v amdgpu.ids

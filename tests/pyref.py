@@ -179,6 +179,27 @@ def densify(us, geom, W, H, ps, st):
     return f
 
 
+def atan2_dis(y, x):
+    """The float atan2 restatement both the oracle and the kernel use (ARM
+    optimized-routines atanf polynomial after reduction to [0, 1])."""
+    f32 = np.float32
+    y = np.asarray(y, f32)
+    x = np.asarray(x, f32)
+    ax, ay = np.abs(x), np.abs(y)
+    mx, mn = np.maximum(ax, ay), np.minimum(ax, ay)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        t = np.where(mx > 0, mn / np.where(mx > 0, mx, f32(1)), f32(0)).astype(f32)
+    z = t * t
+    p = f32(float.fromhex("0x1.01fd88p-8"))
+    for c in ("-0x1.4c3c60p-6", "0x1.93a2c0p-5", "-0x1.491f0ep-4", "0x1.bd7368p-4", "-0x1.24051ep-3",
+              "0x1.99935ep-3", "-0x1.55555p-2"):
+        p = p * z + f32(float.fromhex(c))
+    r = t + (t * z) * p
+    r = np.where(ay > ax, f32(1.57079637) - r, r)
+    r = np.where((x < 0) | ((x == 0) & np.signbit(x)), f32(3.14159274) - r, r)
+    return np.where(np.signbit(y), -r, r).astype(f32)
+
+
 def flow_color(flow, maxmotion=-1.0):
     """Vectorised float32 restatement of draw_optical_flow / compute_color
     (src/color_coding.cpp:13-117), independent of the C oracle."""
@@ -210,7 +231,7 @@ def flow_color(flow, maxmotion=-1.0):
         fx = np.where(ok, x, f32(0)) / f32(maxrad)
         fy = np.where(ok, y, f32(0)) / f32(maxrad)
         rad = np.sqrt(fx * fx + fy * fy)
-        a = np.arctan2(-fy.astype(np.float64), -fx.astype(np.float64)).astype(f32) / f32(3.14159274)
+        a = atan2_dis(-fy, -fx) / f32(3.14159274)
         fk = (a + f32(1)) / f32(2) * f32(ncols - 1)
         k0 = fk.astype(np.int64)
         k1 = (k0 + 1) % ncols

@@ -49,6 +49,8 @@ def main():
         opts = dict(kv.partition("=")[::2] for kv in filter(None, opt.split(",")))
         if "iters" in opts:
             p.iterations = int(opts.pop("iters"))
+        if "vr" in opts:
+            p.var_refine_iters = int(opts.pop("vr"))
         eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
         for k, val in opts.items():
             if k == "streams":

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Throughput of the BASELINE.json configs beyond the headline bench line
+(bench.py measures config 2): one JSON line per config, inputs and outputs
+resident in HBM, batch per call as given, `steps` timed calls after warmup.
+
+  config 1  640x480    ULTRAFAST
+  config 2  1920x1080  MEDIUM            (as bench.py)
+  config 3  3840x2160  MEDIUM
+  config 5  3840x2160  SLOW + variational refinement (3 fixed-point iterations per level)
+  colour    1920x1080  Middlebury colour coding of 32 flow fields (dis_flow_color)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "optical-flow-using-dense-inverse-search_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import disflow  # noqa: E402
+
+CONFIGS = {
+    "1": ("640x480 ULTRAFAST", 640, 480, "ULTRAFAST", 64),
+    "2": ("1920x1080 MEDIUM", 1920, 1080, "MEDIUM", 32),
+    "3": ("3840x2160 MEDIUM", 3840, 2160, "MEDIUM", 8),
+    "5": ("3840x2160 SLOW + variational refinement", 3840, 2160, "SLOW", 2),
+}
+
+
+def run(name, W, H, preset, B, steps, warmup):
+    dev = torch.device("cuda", 0)
+    p = disflow.preset_params(disflow.Preset[preset], W, H)
+    pairs = [disflow.synth_pair(k, W, H) for k in range(B)]
+    d0 = torch.from_numpy(np.stack([a for a, _ in pairs])).to(dev)
+    d1 = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
+    out = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
+    eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    wl = disflow.workload(p, W, H)
+    eng.close()
+    return {"config": name, "preset": preset, "knobs": {"C": p.coarsest_scale, "F": p.finest_scale,
+                                                        "it": p.iterations, "overlap": p.patch_overlap,
+                                                        "var_refine_iters": p.var_refine_iters},
+            "batch": B, "steps": steps, "ms_per_step": el / steps * 1e3, "pairs_per_s": B * steps / el,
+            "patches_per_pair": wl["patches"], "updates_per_pair": wl["updates"],
+            "updates_per_s": wl["updates"] * B * steps / el}
+
+
+def run_colour(steps, warmup):
+    W, H, B = 1920, 1080, 32
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(0)
+    f = torch.from_numpy((rng.standard_normal((B, H, W, 2)) * 4).astype(np.float32)).to(dev)
+    out = torch.empty((B, H, W, 3), dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev)
+    L = disflow.lib()
+
+    def call():
+        disflow._check(L.dis_flow_color(f.data_ptr(), B, W, H, -1.0, out.data_ptr(), disflow.MEM_DEVICE,
+                                        s.cuda_stream, 0))
+    for _ in range(warmup):
+        call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    moved = B * W * H * (8 * 2 + 3)  # flow read twice (max radius, colour), BGR written
+    return {"config": "colour 1920x1080 x32", "ms_per_call": el * 1e3, "fields_per_s": B / el,
+            "hbm_gbs": moved / el / 1e9, "hbm_frac": moved / el / 8e12}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,2,3,5,colour")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    for c in a.configs.split(","):
+        if c == "colour":
+            r = run_colour(a.steps, a.warmup)
+        else:
+            name, W, H, preset, B = CONFIGS[c]
+            steps = max(2, a.steps // (4 if c == "5" else 1))
+            r = run(f"config {c}: {name}", W, H, preset, B, steps, a.warmup)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
