@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 2
+#define DIS_ABI_VERSION 3
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -63,6 +63,10 @@ typedef struct dis_params {
     int patch_normalization; /* 0/1: mean-normalise the warped patch (src/patch.cpp:264) */
     int var_refine_iters;    /* 0 = the reference (no refinement, README.md:11); > 0: fixed-point iterations of
                                 variational refinement per level (parity unpinned) */
+    int paper_mode;          /* 0 = the reference; 1 = the DIS paper's residual and densification (SURVEY 8f
+                                row 4, not in the reference, parity unpinned): template-subtracted (and, with
+                                normalisation, mean-normalised) residual instead of Q2's warped-patch-only one,
+                                and votes weighted by 1/max(1, |I1(x+u) - I0(x)|) instead of Q6's plain mean */
 } dis_params;
 
 typedef struct dis_ctx dis_ctx;

@@ -8,7 +8,9 @@
 // plus options (after the positionals): --flo (also write OF_<folder>/frame_NNNN.flo,
 // the SaveFlowFile format of src/IO_flow.cpp:56-98, which the reference left
 // commented out at src/main.cpp:137-146), --batch N (pairs per GPU call,
-// default 8; the reference is one pair at a time), --device D.
+// default 8; the reference is one pair at a time), --device D, --paper (the DIS
+// paper's residual and densification; not the reference's),
+// --refine K (K fixed-point iterations of variational refinement, 8f row 1).
 //
 // For img_i in [start, end): reads <folder>/frame_<img_i>.png and frame_<img_i+1>
 // (grayscale, src/main.cpp:118-130), computes the full-resolution flow
@@ -45,7 +47,7 @@ void usage()
                  "3. Add full settings\n"
                  "dis_flow folder start_num_image end_num_image max_iter patch_size coarsest_scale finest_scale "
                  "patch_overlap patch_norm draw_grid\n"
-                 "options: --flo  --batch N  --device D"
+                 "options: --flo  --batch N  --device D  --paper  --refine K"
               << std::endl;
 }
 
@@ -77,6 +79,10 @@ int main(int argc, char** argv)
             batch = std::atoi(argv[++i]);
         } else if (a == "--device" && i + 1 < argc) {
             device = std::atoi(argv[++i]);
+        } else if (a == "--paper") {
+            p.paper_mode = 1;
+        } else if (a == "--refine" && i + 1 < argc) {
+            p.var_refine_iters = std::atoi(argv[++i]);
         } else {
             pos.push_back(a);
         }

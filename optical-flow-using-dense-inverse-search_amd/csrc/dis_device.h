@@ -30,6 +30,23 @@ __device__ __forceinline__ int floordiv_r(int a, float rb)
 // Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
 // (src/patch.cpp:176): pivot on |a10| > |a00| (first index wins ties),
 // l = a_q0 / a_p0 (skipped when the pivot is 0), u11 = a_q1 - l * a_p1.
+// I1 sampled at (X, Y): bilinear, replicate border; the position is first
+// clamped to [-1, W] x [-1, H] (oracle vr_warp: identical expressions).
+__device__ __forceinline__ float bilinear_replicate(const float* __restrict__ I, int W, int H, float X, float Y)
+{
+    X = fminf(fmaxf(X, -1.0f), (float)W);
+    Y = fminf(fmaxf(Y, -1.0f), (float)H);
+    const float fx0 = floorf(X), fy0 = floorf(Y);
+    const int xa = (int)fx0, ya = (int)fy0;
+    const float fx = X - fx0, fy = Y - fy0;
+    const int c0 = clampi(xa, 0, W - 1), c1 = clampi(xa + 1, 0, W - 1);
+    const float* r0 = I + (size_t)clampi(ya, 0, H - 1) * W;
+    const float* r1 = I + (size_t)clampi(ya + 1, 0, H - 1) * W;
+    const float top = (1.0f - fx) * r0[c0] + fx * r0[c1];
+    const float bot = (1.0f - fx) * r1[c0] + fx * r1[c1];
+    return (1.0f - fy) * top + fy * bot;
+}
+
 struct LU2 {
     float u00, u01, l10, u11;
     int swap;

@@ -40,6 +40,7 @@ struct SearchArgs {
     int W, H, steps, npw, nph, offw, offh, n;
     float tmp_lb, tmp_ub_w, tmp_ub_h, outlier;
     int iters, norm;
+    int paper;                 // template-subtracted residual (dis_params.paper_mode)
 };
 
 // Fast patch-size-8 search (dis_search8.hip): gradients fused from the level
@@ -62,6 +63,7 @@ struct Search8Args {
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline
+    int paper;                // template-subtracted residual (k_search8<.., kPaper>)
 };
 
 struct DensifyArgs {
@@ -69,6 +71,11 @@ struct DensifyArgs {
     float2* dense;         // dense flow of the level (pre-offset)
     long long u_stride, dense_stride;
     int W, H, ps, steps, npw, nph, offw, offh;
+    // paper mode: votes weighted by 1/max(1, |I1(x+u) - I0(x)|)
+    const float* img0;     // level planes of pair 0 (pre-offset), pair stride plane_stride
+    const float* img1;
+    long long plane_stride;
+    int paper;
 };
 
 struct UpsampleArgs {

@@ -207,6 +207,28 @@ __global__ void __launch_bounds__(64) k_search_generic(SearchArgs a)
             }
     }
     const LU2 lu = hessian_lu<NP>(gdx, gdy);
+    // paper mode: template part of b = sum(g * (I1n - Tn)),
+    // bt = sum(g * Tn), T = frame-0 level image on the patch (replicate border),
+    // Tn = T - mean(T) with normalisation (oracle patch_search)
+    float bt0 = 0.0f, bt1 = 0.0f;
+    if (a.paper) {
+        const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off + org;
+        const int px = (int)refx, py = (int)refy;
+        const int lo = pad > 0 ? -pad : 0;
+        const int hx = pad > 0 ? W - 1 + pad : W - 1, hy = pad > 0 ? H - 1 + pad : H - 1;
+#pragma unroll
+        for (int j = 0; j < PS; ++j)
+#pragma unroll
+            for (int i = 0; i < PS; ++i)
+                r[j * PS + i] = I0[(long long)clampi(py - HP + j, lo, hy) * rs + clampi(px - HP + i, lo, hx)];
+        if (a.norm) {
+            const float mt = eigen_sum<NP>([&](int i) { return r[i]; }) / (float)NP;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) r[i] = r[i] - mt;
+        }
+        bt0 = eigen_sum<NP>([&](int i) { return gdx[i] * r[i]; });
+        bt1 = eigen_sum<NP>([&](int i) { return gdy[i] * r[i]; });
+    }
 
     float inx = 0.0f, iny = 0.0f;
     if (a.dense_coarse)
@@ -249,8 +271,12 @@ __global__ void __launch_bounds__(64) k_search_generic(SearchArgs a)
     if (!oob(sx, sy)) {  // inverse_search_start (src/patch.cpp:131-153)
         warp(sx, sy);
         for (int counter = 1;; ++counter) {  // src/patch.cpp:165-202
-            const float b0 = eigen_sum<NP>([&](int i) { return gdx[i] * r[i]; });
-            const float b1 = eigen_sum<NP>([&](int i) { return gdy[i] * r[i]; });
+            float b0 = eigen_sum<NP>([&](int i) { return gdx[i] * r[i]; });
+            float b1 = eigen_sum<NP>([&](int i) { return gdy[i] * r[i]; });
+            if (a.paper) {
+                b0 = b0 - bt0;
+                b1 = b1 - bt1;
+            }
             float d0, d1;
             lu2_solve(lu, b0, b1, &d0, &d1);
             u0 = u0 - d0;
@@ -295,13 +321,28 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
     gy1 = gy1 > a.nph - 1 ? a.nph - 1 : gy1;
     const float2* u = a.u + (size_t)pair * a.u_stride;
     float fx = 0.0f, fy = 0.0f, w = 0.0f;
-    for (int gx = gx0; gx <= gx1; ++gx)
-        for (int gy = gy0; gy <= gy1; ++gy) {
-            const float2 v = u[gx * a.nph + gy];
-            fx = fx + v.x * 0.5f;
-            fy = fy + v.y * 0.5f;
-            w = w + 0.5f;
-        }
+    if (a.paper) {  // SURVEY 8f row 4 (oracle densify_paper)
+        const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
+        const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
+        const float i0 = I0[(size_t)y * a.W + x];
+        for (int gx = gx0; gx <= gx1; ++gx)
+            for (int gy = gy0; gy <= gy1; ++gy) {
+                const float2 v = u[gx * a.nph + gy];
+                const float d = bilinear_replicate(I1, a.W, a.H, (float)x + v.x, (float)y + v.y) - i0;
+                const float c = 1.0f / fmaxf(1.0f, fabsf(d));
+                fx = fx + c * v.x;
+                fy = fy + c * v.y;
+                w = w + c;
+            }
+    } else {
+        for (int gx = gx0; gx <= gx1; ++gx)
+            for (int gy = gy0; gy <= gy1; ++gy) {
+                const float2 v = u[gx * a.nph + gy];
+                fx = fx + v.x * 0.5f;
+                fy = fy + v.y * 0.5f;
+                w = w + 0.5f;
+            }
+    }
     if (w > 0) {
         fx = fx / w;
         fy = fy / w;

@@ -193,6 +193,7 @@ dis_status check_params(const dis_params* p, int W, int H)
     if (p->iterations < 0) return fail(DIS_ERR_INVALID_ARGUMENT, "iterations must be >= 0");
     if (p->var_refine_iters < 0 || p->var_refine_iters > 64)
         return fail(DIS_ERR_INVALID_ARGUMENT, "var_refine_iters must be in [0, 64]");
+    if (p->paper_mode != 0 && p->paper_mode != 1) return fail(DIS_ERR_INVALID_ARGUMENT, "paper_mode must be 0 or 1");
     const int sf = 1 << p->coarsest_scale;
     const int Wp = W + ((W % sf) ? sf - W % sf : 0), Hp = H + ((H % sf) ? sf - H % sf : 0);
     if ((Wp >> p->coarsest_scale) < 1 || (Hp >> p->coarsest_scale) < 1)
@@ -285,6 +286,10 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     float2* const dense = c->dense + (size_t)p0 * g.dense_stride;
     const bool fast = g.ps == 8 && c->variant != 1;
     const bool vr = c->p.var_refine_iters > 0;
+    const bool paper = c->p.paper_mode != 0;
+    // every level's dense field is materialised (and seeds the next level) under
+    // refinement and in paper mode (weighted densification needs the images)
+    const bool dense_path = vr || paper;
     if (stage == kStageFront && wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
     if (stage == kStageFront) {
         if (fast && g.C >= 1) {
@@ -350,6 +355,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         a.outlier = (float)g.ps / 2;
         a.iters = g.iters;
         a.norm = g.norm;
+        a.paper = paper ? 1 : 0;
         if (fast) {
             dis::Search8Args b{};
             b.img0 = img0;
@@ -380,7 +386,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
             b.fb_count = fb_count + l;
             b.fb_list = c->fb + c->fb_list_off[sub][l];
-            if (vr && l < g.C) {  // refined dense flows: init from the coarser level's dense field
+            b.paper = paper ? 1 : 0;
+            if (dense_path && l < g.C) {  // init from the coarser level's (refined / weighted) dense field
                 b.dense_coarse = dense + g.lv[l + 1].dense_off;
                 b.dense_stride = g.dense_stride;
             }
@@ -390,8 +397,12 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         }
-        if (fast && !c->debug && !vr) continue;  // the fused output kernel densifies the finest level itself
+        if (fast && !c->debug && !dense_path) continue;  // the fused output kernel densifies the finest level
         dis::DensifyArgs d{};
+        d.img0 = img0 + L.plane_off;
+        d.img1 = img1 + L.plane_off;
+        d.plane_stride = g.plane_stride;
+        d.paper = paper ? 1 : 0;
         d.u = pu + L.u_off;
         d.dense = dense + L.dense_off;
         d.u_stride = g.u_stride;
@@ -466,12 +477,12 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         o.hp = g.ps / 2;
         o.vec_store = ((reinterpret_cast<uintptr_t>(flow) & 15) == 0 && (g.W & 1) == 0) ? 1 : 0;
         o.sc = std::pow(2.0f, (float)g.F);
-        fused_out = dis::output_fits(o) && !vr;  // refined: the finest dense field exists
+        fused_out = dis::output_fits(o) && !dense_path;  // refined / paper: the finest dense field exists
     }
     if (fused_out) {
         DIS_HIP(dis::launch_output(o, n, s, timing(c, 3)));
     } else {
-        if (fast && !c->debug && !vr) {  // the search loop skipped the finest densify: do it here
+        if (fast && !c->debug && !dense_path) {  // the search loop skipped the finest densify: do it here
             const dis::LevelGeom& L = g.lv[g.F];
             dis::DensifyArgs d{};
             d.u = pu + L.u_off;

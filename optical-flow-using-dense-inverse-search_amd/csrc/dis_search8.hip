@@ -303,10 +303,12 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
 }
 
 // The per-patch iteration (src/patch.cpp:156-203) with a given tap source.
-template <int LPP, bool kFence, typename TapAt>
+// kPaper: b -= (bt0, bt1), the template part of the
+// template-subtracted residual (see search_block).
+template <int LPP, bool kFence, bool kPaper, typename TapAt>
 __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[8 * kNCol<LPP>],
                                         const float (&gy)[8 * kNCol<LPP>], float rx, float ry, float ix, float iy,
-                                        float* pu0, float* pu1, TapAt&& tap_at)
+                                        float bt0, float bt1, float* pu0, float* pu1, TapAt&& tap_at)
 {
     float u0 = ix, u1 = iy;
     const float sx = rx + u0, sy = ry + u1;
@@ -317,8 +319,12 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
     for (int counter = 1;; ++counter) {
         const Warp w = warp_coefs(px, py);
         warp_patch<LPP, kFence>(w, a.norm, tap_at(w), r);
-        const float b0 = patch_dot<LPP>(gx, [&](int j) { return r[j]; });
-        const float b1 = patch_dot<LPP>(gy, [&](int j) { return r[j]; });
+        float b0 = patch_dot<LPP>(gx, [&](int j) { return r[j]; });
+        float b1 = patch_dot<LPP>(gy, [&](int j) { return r[j]; });
+        if constexpr (kPaper) {
+            b0 = b0 - bt0;
+            b1 = b1 - bt1;
+        }
         float d0, d1;
         lu2_solve(lu, b0, b1, &d0, &d1);
         u0 = u0 - d0;
@@ -361,7 +367,7 @@ struct BlockLds {
 // is appended to the launch's fallback list (a.fb_count / a.fb_list) for
 // k_search8_fb and nothing is written here (keeps this kernel's registers
 // low enough for 4 waves per SIMD at LPP 2).
-template <int LPP, bool kFallback>
+template <int LPP, bool kFallback, bool kPaper>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -507,6 +513,29 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
         for (int j = 0; j < 8 * NC; ++j) gdx[j] = gdy[j] = 0.0f;
     }
+    // paper mode (oracle patch_search): bt = sum(g * Tn) in the
+    // Eigen order, T = the level image on the patch with the replicate border
+    // (clamped pixel, which the staged region holds), Tn = T - mean(T) with
+    // normalisation
+    float bt0 = 0.0f, bt1 = 0.0f;
+    if constexpr (kPaper) {
+        if (active) {
+            float tv[8 * NC];
+#pragma unroll
+            for (int ci = 0; ci < NC; ++ci) {
+                const int cx = clampi(irx - 4 + lane_col<LPP>(q, ci), 0, W - 1) - x0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) tv[8 * ci + j] = tile[(clampi(iry - 4 + j, 0, H - 1) - y0) * RS + cx];
+            }
+            if (a.norm) {
+                const float mt = patch_sum<LPP>(tv) / 64.0f;
+#pragma unroll
+                for (int j = 0; j < 8 * NC; ++j) tv[j] = tv[j] - mt;
+            }
+            bt0 = patch_dot<LPP>(gdx, [&](int j) { return tv[j]; });
+            bt1 = patch_dot<LPP>(gdy, [&](int j) { return tv[j]; });
+        }
+    }
 
     // --- 3. initialisation from the coarser level (src/patch_grid.cpp:108-119):
     // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
@@ -595,7 +624,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         __syncthreads();
         if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
-            iterate<LPP, false>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+            iterate<LPP, false, kPaper>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
                 return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
@@ -603,7 +632,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     } else if constexpr (kFallback) {
         if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
-            iterate<LPP, true>(a, lu, gdx, gdy, rx, ry, ix, iy, &u0, &u1, [&](const Warp& w) {
+            iterate<LPP, true, kPaper>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
                 const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
                 return [=](int k, int c) {
                     return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
@@ -622,12 +651,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 }
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
-template <int LPP, bool kFallback>
+template <int LPP, bool kFallback, bool kPaper = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
-    search_block<LPP, kFallback>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+    search_block<LPP, kFallback, kPaper>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
@@ -635,7 +664,7 @@ k_search8(Search8Args a)
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
 // its workgroups cannot take the slots another stream's search kernel frees,
 // and the (usually empty) launch waited 70-150 us for that kernel to drain.
-template <int LPP>
+template <int LPP, bool kPaper = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
 __attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
@@ -646,7 +675,7 @@ k_search8_fb(Search8Args a)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int e = a.fb_list[i];
         const int bx = e % nbx, t = e / nbx;
-        search_block<LPP, true>(a, bx, t % nby, t / nby, S);
+        search_block<LPP, true, kPaper>(a, bx, t % nby, t / nby, S);
         __syncthreads();  // LDS reuse by the next listed block
     }
 }
@@ -689,6 +718,31 @@ bool search8_lpp1_fits(int steps)
     return (15 * steps + 11) * (7 * steps + 10) <= kTileH * kTSMax<1>;
 }
 
+template <bool kPaper>
+static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid, dim3 fb_grid, hipStream_t s,
+                             Timing t)
+{
+    if (L == 1) {
+        if (split) {
+            DIS_LAUNCH(t, (k_search8<1, false, kPaper>), grid, dim3(kThreads<1>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<1, kPaper>), fb_grid, dim3(kThreads<1>), 0, s, a);
+        } else {
+            DIS_LAUNCH(t, (k_search8<1, true, kPaper>), grid, dim3(kThreads<1>), 0, s, a);
+        }
+    } else if (L == 2) {
+        if (split) {
+            DIS_LAUNCH(t, (k_search8<2, false, kPaper>), grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, kPaper>), fb_grid, dim3(kThreads<2>), 0, s, a);
+        } else {
+            DIS_LAUNCH(t, (k_search8<2, true, kPaper>), grid, dim3(kThreads<2>), 0, s, a);
+        }
+    } else if (L == 4) {
+        DIS_LAUNCH(t, (k_search8<4, true, kPaper>), grid, dim3(kThreads<4>), 0, s, a);
+    } else {
+        DIS_LAUNCH(t, (k_search8<8, true, kPaper>), grid, dim3(kThreads<8>), 0, s, a);
+    }
+}
+
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t)
 {
     const int L = a.lanes_per_patch;
@@ -702,25 +756,10 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     const bool split = (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
-    if (L == 1) {
-        if (split) {
-            DIS_LAUNCH(t, (k_search8<1, false>), grid, dim3(kThreads<1>), 0, s, a);
-            hipLaunchKernelGGL(k_search8_fb<1>, fb_grid, dim3(kThreads<1>), 0, s, a);
-        } else {
-            DIS_LAUNCH(t, (k_search8<1, true>), grid, dim3(kThreads<1>), 0, s, a);
-        }
-    } else if (L == 2) {
-        if (split) {
-            DIS_LAUNCH(t, (k_search8<2, false>), grid, dim3(kThreads<2>), 0, s, a);
-            hipLaunchKernelGGL(k_search8_fb<2>, fb_grid, dim3(kThreads<2>), 0, s, a);
-        } else {
-            DIS_LAUNCH(t, (k_search8<2, true>), grid, dim3(kThreads<2>), 0, s, a);
-        }
-    } else if (L == 4) {
-        DIS_LAUNCH(t, (k_search8<4, true>), grid, dim3(kThreads<4>), 0, s, a);
-    } else {
-        DIS_LAUNCH(t, (k_search8<8, true>), grid, dim3(kThreads<8>), 0, s, a);
-    }
+    if (a.paper)
+        launch_search8_t<true>(a, L, split, grid, fb_grid, s, t);
+    else
+        launch_search8_t<false>(a, L, split, grid, fb_grid, s, t);
     return hipGetLastError();
 }
 

@@ -81,6 +81,7 @@ class _Params(ctypes.Structure):
         ("patch_overlap", ctypes.c_float),
         ("patch_normalization", ctypes.c_int),
         ("var_refine_iters", ctypes.c_int),
+        ("paper_mode", ctypes.c_int),
     ]
 
 
@@ -109,15 +110,17 @@ class Params:
     patch_overlap: float = 0.625
     patch_normalization: int = 1
     var_refine_iters: int = 0
+    paper_mode: int = 0
 
     def _c(self) -> _Params:
         return _Params(self.coarsest_scale, self.finest_scale, self.patch_size, self.iterations,
-                       self.patch_overlap, int(self.patch_normalization), self.var_refine_iters)
+                       self.patch_overlap, int(self.patch_normalization), self.var_refine_iters,
+                       int(self.paper_mode))
 
     @staticmethod
     def _from_c(p: _Params) -> "Params":
         return Params(p.coarsest_scale, p.finest_scale, p.patch_size, p.iterations,
-                      float(p.patch_overlap), p.patch_normalization, p.var_refine_iters)
+                      float(p.patch_overlap), p.patch_normalization, p.var_refine_iters, p.paper_mode)
 
 
 _lib = None

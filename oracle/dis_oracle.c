@@ -235,6 +235,8 @@ typedef struct {
     /* image_parameters (include/optical_flow.hpp:24-34) */
     int width, height, pad, tmp_w;
     float tmp_lb, tmp_ub_w, tmp_ub_h;
+    /* SURVEY 8f row 4 (not in the reference): DIS-paper residual */
+    int paper;
 } level_ctx;
 
 /* Patch::get_patch_second_image (src/patch.cpp:207-267). */
@@ -280,7 +282,7 @@ static int out_of_bounds(const level_ctx* c, float x, float y)
 }
 
 /* Patch::init_patch + Patch::inverse_search for one patch; returns u. */
-static void patch_search(const level_ctx* c, const float* dxp, const float* dyp,
+static void patch_search(const level_ctx* c, const float* imgp, const float* dxp, const float* dyp,
                          const float* img_second, float refx, float refy,
                          float initx, float inity, float* gdx, float* gdy,
                          float* second, float* ux, float* uy)
@@ -306,6 +308,27 @@ static void patch_search(const level_ctx* c, const float* dxp, const float* dyp,
     if (h[0] * h[3] - h[2] * h[1] == 0.0f) {   /* Eigen 2x2 determinant, :86 */
         h[0] = (float)((double)h[0] + 1e-10);  /* float += double literal, :88 */
         h[3] = (float)((double)h[3] + 1e-10);  /* :89 */
+    }
+    /* Paper mode (Kroeger et al. 2016 eq. 3, fixes Q2): the
+     * residual is template-subtracted, r = (I1w - mean I1w) - (T - mean T)
+     * (means only with normalisation), T = the frame-0 level image on the
+     * patch (patch_grad, src/patch.cpp:68, which the reference never uses).
+     * Since sum(g*(I1n - Tn)) = sum(g*I1n) - sum(g*Tn), the template part is a
+     * per-patch constant: b = sum(g*I1n) - bt with bt = sum(g*Tn), both sums
+     * in the Eigen order. This split IS the definition the kernels follow. */
+    float bt0 = 0.0f, bt1 = 0.0f;
+    if (c->paper) {
+        float tn[1024], tmp[1024];
+        for (int j = lb, q2 = 0; j <= ub; ++j)
+            for (int i = lb; i <= ub; ++i, ++q2) tn[q2] = imgp[(posx + i) + (posy + j) * c->tmp_w];
+        if (c->normalization) {
+            const float mt = eigen_sum(tn, c->npts) / (float)c->npts;
+            for (int i = 0; i < c->npts; ++i) tn[i] = tn[i] - mt;
+        }
+        for (int i = 0; i < c->npts; ++i) tmp[i] = gdx[i] * tn[i];
+        bt0 = eigen_sum(tmp, c->npts);
+        for (int i = 0; i < c->npts; ++i) tmp[i] = gdy[i] * tn[i];
+        bt1 = eigen_sum(tmp, c->npts);
     }
 
     /* inverse_search_start (src/patch.cpp:119-154), after reset_patch (:102-116) */
@@ -333,6 +356,10 @@ static void patch_search(const level_ctx* c, const float* dxp, const float* dyp,
             for (int i = 0; i < c->npts; ++i) tmp[i] = gdy[i] * second[i];
             b1 = eigen_sum(tmp, c->npts);                       /* :172 */
         }
+        if (c->paper) {                                         /* template part (paper mode) */
+            b0 = b0 - bt0;
+            b1 = b1 - bt1;
+        }
         float d0, d1;
         eigen_lu_solve2(h, b0, b1, &d0, &d1);                   /* :176 */
         u0 = u0 - d0;                                           /* :179 */
@@ -359,6 +386,46 @@ static void patch_search(const level_ctx* c, const float* dxp, const float* dyp,
 /* ------------------------------------------------------------------------- */
 /* a14: densification (src/patch_grid.cpp:121-182)                           */
 /* ------------------------------------------------------------------------- */
+
+static float vr_warp(const float* I1, int stride, int W, int H, float X, float Y);
+
+/* Paper mode (Kroeger et al. 2016 eq. 4, fixes Q6): each
+ * covering patch's vote is weighted by 1 / max(1, |I1(x + u) - I0(x)|), with
+ * I1 bilinear, replicate border (vr_warp), on the level images; contributions
+ * in patch-id order, f = ((f + w*u) ...) / (sum of w). */
+static void densify_paper(const level_ctx* c, int npw, int nph, int steps, int offw, int offh,
+                          const float* patch_u, const float* I0, const float* I1, int stride, float* dense)
+{
+    const int W = c->width, H = c->height;
+    float* weight = (float*)calloc((size_t)W * H, sizeof(float));
+    memset(dense, 0, sizeof(float) * 2 * (size_t)W * H);
+    int lb = -c->ps / 2, ub = c->ps / 2 - 1;
+    for (int gx = 0; gx < npw; ++gx)
+        for (int gy = 0; gy < nph; ++gy) {
+            const int ip = gx * nph + gy;
+            const int rx = gx * steps + offw, ry = gy * steps + offh;
+            const float u0 = patch_u[2 * ip], u1 = patch_u[2 * ip + 1];
+            for (int y = lb; y <= ub; ++y)
+                for (int x = lb; x <= ub; ++x) {
+                    int xt = x + rx, yt = y + ry;
+                    if (xt >= 0 && yt >= 0 && xt < W && yt < H) {
+                        size_t i = (size_t)yt * W + xt;
+                        const float d = vr_warp(I1, stride, W, H, (float)xt + u0, (float)yt + u1) -
+                                        I0[(size_t)yt * stride + xt];
+                        const float w = 1.0f / fmaxf(1.0f, fabsf(d));
+                        weight[i] = weight[i] + w;
+                        dense[2 * i] = dense[2 * i] + w * u0;
+                        dense[2 * i + 1] = dense[2 * i + 1] + w * u1;
+                    }
+                }
+        }
+    for (size_t i = 0; i < (size_t)W * H; ++i)
+        if (weight[i] > 0) {
+            dense[2 * i] = dense[2 * i] / weight[i];
+            dense[2 * i + 1] = dense[2 * i + 1] / weight[i];
+        }
+    free(weight);
+}
 
 static void densify(const level_ctx* c, int npw, int nph, int steps, int offw, int offh,
                     const float* patch_u, float* dense)
@@ -616,16 +683,16 @@ int dis_oracle_flow_from_pyramids(
     int patch_size, float patch_overlap, int patch_normalization,
     float* dbg_patch_u, float* dbg_dense)
 {
-    return dis_oracle_flow_from_pyramids_vr(img_first, img_first_dx, img_first_dy, img_second, img_padding, outflow,
+    return dis_oracle_flow_from_pyramids_ex(img_first, img_first_dx, img_first_dy, img_second, img_padding, outflow,
                                             width, height, coarsest, finest, iterations, patch_size, patch_overlap,
-                                            patch_normalization, 0, dbg_patch_u, dbg_dense);
+                                            patch_normalization, 0, 0, dbg_patch_u, dbg_dense);
 }
 
-int dis_oracle_flow_from_pyramids_vr(
+int dis_oracle_flow_from_pyramids_ex(
     float* const* img_first, float* const* img_first_dx, float* const* img_first_dy,
     float* const* img_second, int img_padding, float* outflow,
     int width, int height, int coarsest, int finest, int iterations,
-    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters,
+    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters, int paper_mode,
     float* dbg_patch_u, float* dbg_dense)
 {
     if (patch_size < 2 || (patch_size & 1) || patch_size * patch_size > 1024) return -1;
@@ -652,6 +719,7 @@ int dis_oracle_flow_from_pyramids_vr(
         c.tmp_ub_w = (float)(c.width + patch_size / 2 - 2);      /* :56 */
         c.tmp_ub_h = (float)(c.height + patch_size / 2 - 2);     /* :57 */
         c.tmp_w = c.width + 2 * img_padding;                     /* :58 */
+        c.paper = paper_mode;
 
         int npw, nph, offw, offh;
         dis_oracle_grid(c.width, c.height, steps, &npw, &nph, &offw, &offh);
@@ -670,10 +738,15 @@ int dis_oracle_flow_from_pyramids_vr(
                     ix = flows[scale + 1][2 * i] * 2;
                     iy = flows[scale + 1][2 * i + 1] * 2;
                 }
-                patch_search(&c, img_first_dx[scale], img_first_dy[scale], img_second[scale],
+                patch_search(&c, img_first[scale], img_first_dx[scale], img_first_dy[scale], img_second[scale],
                              rx, ry, ix, iy, gdx, gdy, second, &pu[2 * ip], &pu[2 * ip + 1]);
             }
-        densify(&c, npw, nph, steps, offw, offh, pu, dense);     /* :86-90 */
+        if (paper_mode)                                          /* SURVEY 8f row 4 */
+            densify_paper(&c, npw, nph, steps, offw, offh, pu,
+                          img_first[scale] + (size_t)img_padding * c.tmp_w + img_padding,
+                          img_second[scale] + (size_t)img_padding * c.tmp_w + img_padding, c.tmp_w, dense);
+        else
+            densify(&c, npw, nph, steps, offw, offh, pu, dense); /* :86-90 */
         if (var_refine_iters > 0)                                /* SURVEY 8f row 1 (not in the reference) */
             dis_oracle_var_refine(img_first[scale] + (size_t)img_padding * c.tmp_w + img_padding,
                                   img_second[scale] + (size_t)img_padding * c.tmp_w + img_padding, c.tmp_w,
@@ -834,9 +907,10 @@ int dis_oracle_calc_u8(const dis_oracle_params* p, int W, int H,
         off += (size_t)w * h;
     }
     float* flowF = (float*)malloc(sizeof(float) * 2 * (size_t)(Wp >> F) * (Hp >> F));
-    int rc = dis_oracle_flow_from_pyramids_vr(P0, PX, PY, P1, ps, flowF, Wp, Hp, C, F,
+    int rc = dis_oracle_flow_from_pyramids_ex(P0, PX, PY, P1, ps, flowF, Wp, Hp, C, F,
                                            p->iterations, ps, p->patch_overlap,
-                                           p->patch_normalization, p->var_refine_iters, NULL, NULL);
+                                           p->patch_normalization, p->var_refine_iters, p->paper_mode,
+                                           NULL, NULL);
     if (rc == 0) dis_oracle_upsample_crop(flowF, Wp, Hp, F, pl, pt, W, H, flow_out);
     for (int l = 0; l <= C; ++l) { free(P0[l]); free(PX[l]); free(PY[l]); free(P1[l]); }
     free(flowF); free(f0); free(f1); free(img0); free(dx0); free(dy0); free(img1);

@@ -32,6 +32,7 @@ typedef struct {
     float patch_overlap;     /* src/optical_flow.cpp:490 */
     int patch_normalization; /* include/optical_flow.hpp:43 */
     int var_refine_iters;    /* 0 = the reference (no refinement) */
+    int paper_mode;          /* 0 = the reference; 1 = DIS-paper residual + weighted densify */
 } dis_oracle_params;
 
 /* Grid geometry of one level (src/optical_flow.cpp:490, src/patch_grid.cpp:20-23). */
@@ -70,13 +71,15 @@ int dis_oracle_flow_from_pyramids(
     float* dbg_patch_u, float* dbg_dense);
 
 /* As above, plus `var_refine_iters` fixed-point iterations of variational
- * refinement on each level's dense flow after densification (SURVEY 8f row 1;
- * absent from the reference: parity unpinned). 0 = the reference. */
-int dis_oracle_flow_from_pyramids_vr(
+ * refinement on each level's dense flow after densification
+ * and `paper_mode` (template-subtracted residual and
+ * residual-weighted densification, Kroeger et al. 2016 eqs. 3-4). Both are
+ * absent from the reference (parity unpinned); 0, 0 = the reference. */
+int dis_oracle_flow_from_pyramids_ex(
     float* const* img_first, float* const* img_first_dx, float* const* img_first_dy,
     float* const* img_second, int img_padding, float* outflow,
     int width, int height, int coarsest, int finest, int iterations,
-    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters,
+    int patch_size, float patch_overlap, int patch_normalization, int var_refine_iters, int paper_mode,
     float* dbg_patch_u, float* dbg_dense);
 
 /* Variational refinement of one level's dense flow (W*H*2, in place) between

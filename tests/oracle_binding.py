@@ -23,6 +23,7 @@ class Params(ctypes.Structure):
         ("patch_overlap", ctypes.c_float),
         ("patch_normalization", ctypes.c_int),
         ("var_refine_iters", ctypes.c_int),
+        ("paper_mode", ctypes.c_int),
     ]
 
 
@@ -45,6 +46,8 @@ def _load():
     L.dis_oracle_var_energy.restype = ctypes.c_double
     L.dis_oracle_flow_from_pyramids.argtypes = [P(V)] * 4 + [I, V, I, I, I, I, I, I, F, I, V, V]
     L.dis_oracle_flow_from_pyramids.restype = I
+    L.dis_oracle_flow_from_pyramids_ex.argtypes = [P(V)] * 4 + [I, V, I, I, I, I, I, I, F, I, I, I, V, V]
+    L.dis_oracle_flow_from_pyramids_ex.restype = I
     L.dis_oracle_upsample_crop.argtypes = [V, I, I, I, I, I, I, I, V]
     L.dis_oracle_calc_u8.argtypes = [P(Params), I, I, V, V, Z, V]
     L.dis_oracle_calc_u8.restype = I
@@ -118,7 +121,7 @@ def pad_planes(planes, pad, mode):
     return [np.ascontiguousarray(np.pad(p, pad, mode=mode), dtype=np.float32) for p in planes]
 
 
-def flow_from_pyramids(P0, PX, PY, P1, pad, W, H, C, F, it, ps, overlap, norm, capture=False):
+def flow_from_pyramids(P0, PX, PY, P1, pad, W, H, C, F, it, ps, overlap, norm, capture=False, vr=0, paper=0):
     nl = C + 1
 
     def arr(lst):
@@ -132,12 +135,12 @@ def flow_from_pyramids(P0, PX, PY, P1, pad, W, H, C, F, it, ps, overlap, norm, c
         nd = sum((W >> l) * (H >> l) for l in range(nl))
         dbg_u = np.full(2 * nu, np.nan, np.float32)
         dbg_d = np.full(2 * nd, np.nan, np.float32)
-    rc = lib.dis_oracle_flow_from_pyramids(
+    rc = lib.dis_oracle_flow_from_pyramids_ex(
         ctypes.cast(arr(P0), ctypes.POINTER(ctypes.c_void_p)),
         ctypes.cast(arr(PX), ctypes.POINTER(ctypes.c_void_p)),
         ctypes.cast(arr(PY), ctypes.POINTER(ctypes.c_void_p)),
         ctypes.cast(arr(P1), ctypes.POINTER(ctypes.c_void_p)),
-        pad, _p(out), W, H, C, F, it, ps, overlap, int(norm), _p(dbg_u), _p(dbg_d))
+        pad, _p(out), W, H, C, F, it, ps, overlap, int(norm), int(vr), int(paper), _p(dbg_u), _p(dbg_d))
     assert rc == 0
     if not capture:
         return out
@@ -159,9 +162,9 @@ def upsample_crop(flowF, Wp, Hp, F, pl, pt, W, H):
     return out
 
 
-def calc_u8(I0, I1, C, F, ps, it, overlap, norm=1, vr=0):
+def calc_u8(I0, I1, C, F, ps, it, overlap, norm=1, vr=0, paper=0):
     H, W = I0.shape
-    p = Params(C, F, ps, it, overlap, norm, vr)
+    p = Params(C, F, ps, it, overlap, norm, vr, paper)
     out = np.empty((H, W, 2), np.float32)
     a0 = np.ascontiguousarray(I0, dtype=np.uint8)
     a1 = np.ascontiguousarray(I1, dtype=np.uint8)
@@ -174,7 +177,7 @@ def calc_from_params(I0, I1, params):
     """params: disflow.Params (or anything with the same attributes)."""
     return calc_u8(I0, I1, params.coarsest_scale, params.finest_scale, params.patch_size,
                    params.iterations, params.patch_overlap, params.patch_normalization,
-                   getattr(params, "var_refine_iters", 0))
+                   getattr(params, "var_refine_iters", 0), getattr(params, "paper_mode", 0))
 
 
 def build_pyramids(I0, I1, C, ps):

@@ -91,8 +91,10 @@ def lu_solve(h00, h01, h10, h11, b0, b1):
     return c0, c1
 
 
-def search_level(dxp, dyp, I1p, pad, W, H, ps, st, it, norm, init):
-    """One PatchGrid level over padded planes; init: dict id -> (u, v) or None."""
+def search_level(dxp, dyp, I1p, pad, W, H, ps, st, it, norm, init, I0p=None):
+    """One PatchGrid level over padded planes; init: dict id -> (u, v) or None.
+    I0p (padded frame-0 level image) given: paper mode,
+    b = sum(g*I1n) - sum(g*Tn) with Tn the (mean-normalised) template."""
     npw = int(math.ceil(f32(W) / f32(st)))
     nph = int(math.ceil(f32(H) / f32(st)))
     offw = (W - (npw - 1) * st) // 2
@@ -117,6 +119,12 @@ def search_level(dxp, dyp, I1p, pad, W, H, ps, st, it, norm, init):
             if h00 * h11 - h10 * h01 == 0:
                 h00 = f32(float(h00) + 1e-10)
                 h11 = f32(float(h11) + 1e-10)
+            bt0 = bt1 = None
+            if I0p is not None:
+                tn = I0p[py - hp:py + hp, px - hp:px + hp].reshape(-1).astype(f32)
+                if norm:
+                    tn = tn - eigen_sum(tn) / f32(ps * ps)
+                bt0, bt1 = eigen_sum(gdx * tn), eigen_sum(gdy * tn)
             iu, iv = init(pid, rx, ry) if init else (f32(0), f32(0))
             u0, u1 = iu, iv
             sx, sy = rx + u0, ry + u1
@@ -146,6 +154,8 @@ def search_level(dxp, dyp, I1p, pad, W, H, ps, st, it, norm, init):
                     counter += 1
                     b0 = eigen_sum(gdx * r)
                     b1 = eigen_sum(gdy * r)
+                    if bt0 is not None:
+                        b0, b1 = b0 - bt0, b1 - bt1
                     d0, d1 = lu_solve(h00, h01, h10, h11, b0, b1)
                     u0, u1 = u0 - d0, u1 - d1
                     qx, qy = rx + u0, ry + u1
@@ -174,6 +184,46 @@ def densify(us, geom, W, H, ps, st):
             y0, y1 = max(ry - hp, 0), min(ry + hp, H)
             w[y0:y1, x0:x1] = w[y0:y1, x0:x1] + f32(0.5)
             f[y0:y1, x0:x1] = f[y0:y1, x0:x1] + u
+    m = w > 0
+    f[m] = f[m] / w[m][:, None]
+    return f
+
+
+def bilinear_replicate(I, X, Y):
+    """I sampled at float32 arrays (X, Y): bilinear, replicate border, the
+    position clamped to [-1, W] x [-1, H] first."""
+    H, W = I.shape
+    X = np.minimum(np.maximum(X, f32(-1)), f32(W)).astype(f32)
+    Y = np.minimum(np.maximum(Y, f32(-1)), f32(H)).astype(f32)
+    fx0, fy0 = np.floor(X), np.floor(Y)
+    xa, ya = fx0.astype(np.int64), fy0.astype(np.int64)
+    fx, fy = X - fx0, Y - fy0
+    c0, c1 = np.clip(xa, 0, W - 1), np.clip(xa + 1, 0, W - 1)
+    r0, r1 = np.clip(ya, 0, H - 1), np.clip(ya + 1, 0, H - 1)
+    top = (f32(1) - fx) * I[r0, c0] + fx * I[r0, c1]
+    bot = (f32(1) - fx) * I[r1, c0] + fx * I[r1, c1]
+    return ((f32(1) - fy) * top + fy * bot).astype(f32)
+
+
+def densify_paper(us, geom, I0, I1, W, H, ps, st):
+    """Paper-mode densification: votes weighted by
+    1 / max(1, |I1(x + u) - I0(x)|), patch-id order; I0/I1 unpadded level images."""
+    npw, nph, offw, offh = geom
+    f = np.zeros((H, W, 2), f32)
+    w = np.zeros((H, W), f32)
+    hp = ps // 2
+    for gx in range(npw):
+        for gy in range(nph):
+            u = us[gx * nph + gy]
+            rx, ry = gx * st + offw, gy * st + offh
+            x0, x1 = max(rx - hp, 0), min(rx + hp, W)
+            y0, y1 = max(ry - hp, 0), min(ry + hp, H)
+            yy, xx = np.mgrid[y0:y1, x0:x1]
+            d = bilinear_replicate(I1, xx.astype(f32) + u[0], yy.astype(f32) + u[1]) - I0[y0:y1, x0:x1]
+            c = (f32(1) / np.maximum(f32(1), np.abs(d))).astype(f32)
+            w[y0:y1, x0:x1] = w[y0:y1, x0:x1] + c
+            f[y0:y1, x0:x1, 0] = f[y0:y1, x0:x1, 0] + c * u[0]
+            f[y0:y1, x0:x1, 1] = f[y0:y1, x0:x1, 1] + c * u[1]
     m = w > 0
     f[m] = f[m] / w[m][:, None]
     return f

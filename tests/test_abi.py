@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(disflow_mod):
     L = disflow_mod.lib()
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert L.dis_abi_version() == 2
+    assert L.dis_abi_version() == 3
 
 
 def test_no_oracle_linked_into_product(disflow_mod):
@@ -62,6 +62,8 @@ def test_presets(disflow_mod):
     ("iterations", -1, -1),
     ("var_refine_iters", 65, -1),  # refinement iterations in [0, 64]
     ("var_refine_iters", -1, -1),
+    ("paper_mode", 2, -1),        # 0 = the reference, 1 = DIS-paper residual / densification
+    ("paper_mode", -1, -1),
 ])
 def test_validation_errors(disflow_mod, field, value, status):
     p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, 1920, 1080)

@@ -109,3 +109,22 @@ def test_cli_sequence_matches_oracle(tools, tmp_path, disflow_mod, oracle):
         assert np.array_equal(flo.view(np.uint32), exp.view(np.uint32)), f"flow {i}"
         rgb = pngio.read_rgb8(str(tmp_path / f"OF_seq/frame_{i:04d}.png"))
         assert np.array_equal(rgb, oracle.flow_color(exp)[..., ::-1]), f"colour {i}"
+
+
+@pytest.mark.gpu
+def test_cli_paper_and_refine_options(tools, tmp_path, disflow_mod, oracle):
+    # --paper and --refine K (8f row 1) reach dis_params
+    W, H = 128, 96
+    I0, I1 = disflow_mod.synth_pair(57, W, H)
+    d = tmp_path / "pp"
+    d.mkdir()
+    pngio.write_gray8(str(d / "frame_0001.png"), I0)
+    pngio.write_gray8(str(d / "frame_0002.png"), I1)
+    args = [CLI, "pp", "1", "2", "8", "8", "3", "0", "0.5", "1", "0", "--flo", "--paper", "--refine", "2"]
+    r = subprocess.run(args, capture_output=True, text=True, cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    p = disflow_mod.Params(coarsest_scale=3, finest_scale=0, patch_size=8, iterations=8, patch_overlap=0.5,
+                           patch_normalization=1, var_refine_iters=2, paper_mode=1)
+    exp = oracle.calc_from_params(I0, I1, p)
+    flo = disflow_mod.read_flo(str(tmp_path / "OF_pp/frame_0001.flo"))
+    assert np.array_equal(flo.view(np.uint32), exp.view(np.uint32))

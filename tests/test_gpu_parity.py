@@ -335,3 +335,61 @@ def test_slow_preset_with_refinement_bitexact(disflow_mod, oracle):
     I0, I1 = disflow_mod.synth_pair(70, W, H)
     got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
     _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "slow + refinement")
+
+
+# --- paper mode (template-subtracted residual, residual-weighted
+# densification). Not in the reference: HIP vs the oracle's restatement, bit-exact.
+
+PAPER_CASES = [
+    # (W, H, preset or knobs, variants)
+    (352, 288, "MEDIUM"),
+    (640, 480, "ULTRAFAST"),
+    (203, 151, (3, 0, 8, 10, 0.7, 1)),    # ragged, F = 0
+    (96, 64, (2, 1, 6, 5, 0.5, 0)),       # generic kernel (ps 6), no normalisation
+    (128, 96, (3, 0, 4, 6, 0.5, 1)),      # generic kernel (ps 4)
+]
+
+
+@pytest.mark.parametrize("W,H,cfg", PAPER_CASES)
+def test_paper_mode_bitexact(disflow_mod, oracle, W, H, cfg):
+    if isinstance(cfg, str):
+        p = disflow_mod.preset_params(disflow_mod.Preset[cfg], W, H)
+    else:
+        p = _params(disflow_mod, *cfg)
+    p.paper_mode = 1
+    I0, I1 = disflow_mod.synth_pair(W + 3 * H, W, H)
+    J0, _ = disflow_mod.synth_pair(W + 3 * H + 1, W, H)
+    exp = oracle.calc_from_params(I0, I1, p)
+    exp_fb = oracle.calc_from_params(J0, I1, p)  # unrelated frames: tile fallback blocks
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    variants = ((0, "auto"), (1, "generic"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1")) \
+        if p.patch_size == 8 else ((0, "auto"),)
+    for variant, name in variants:
+        eng.set_variant(variant)
+        _assert_bitexact(eng.calc(I0, I1), exp, f"paper {name}")
+        _assert_bitexact(eng.calc(J0, I1), exp_fb, f"paper {name} fallback")
+
+
+def test_paper_mode_batch_streams_and_refinement(disflow_mod, oracle):
+    # a batch of 3 on 2 sub-batch streams, with and without refinement on top
+    W, H = 320, 240
+    pairs = [disflow_mod.synth_pair(90 + k, W, H) for k in range(3)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    for vr in (0, 2):
+        p = disflow_mod.Params(coarsest_scale=4, finest_scale=1, patch_size=8, iterations=10,
+                               patch_overlap=0.625, patch_normalization=1, var_refine_iters=vr, paper_mode=1)
+        eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=3)
+        eng.set_concurrency(2)
+        got = eng.calc_batch(I0, I1)
+        for k in range(3):
+            _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"paper vr={vr} pair {k}")
+
+
+def test_paper_mode_identical_frames_zero_flow_on_gpu(disflow_mod):
+    W, H = 160, 120
+    I0, _ = disflow_mod.synth_pair(5, W, H)
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    p.paper_mode = 1
+    got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I0)
+    assert np.array_equal(got, np.zeros_like(got))

@@ -297,3 +297,58 @@ def test_var_refine_improves_synthetic_accuracy(oracle):
             f = oracle.calc_u8(I0, I1, 4, 0, 8, 16, 0.75, 1, vr)
             e[vr].append(np.sqrt(((f - gt) ** 2).sum(-1)).mean())
     assert np.mean(e[3]) < 0.85 * np.mean(e[0])
+
+
+# --- paper mode (DIS-paper residual + weighted densification) --
+# Not in the reference (parity unpinned by construction): the C oracle's
+# restatement is cross-checked by the independent numpy one, plus known answers.
+
+@pytest.mark.parametrize("ps,overlap,it,norm", [(8, 0.625, 4, 1), (4, 0.5, 3, 0), (8, 0.7, 2, 1)])
+def test_paper_mode_matches_numpy(oracle, ps, overlap, it, norm):
+    W, H, C, F = 64, 48, 2, 0
+    I0, I1 = shifted_pair(15, H, W)
+    Wp, Hp, P0, PX, PY, P1, py0, py1 = oracle.build_pyramids(I0, I1, C, ps)
+    out, us, ds = oracle.flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, overlap, norm,
+                                            capture=True, paper=1)
+    st = oracle.steps(ps, overlap)
+    prev = None
+    for l in range(C, F - 1, -1):
+        w, h = Wp >> l, Hp >> l
+        if prev is None:
+            init = None
+        else:
+            def init(pid, rx, ry, prev=prev, w=w):
+                x, y = int(np.floor(rx / f32(2))), int(np.floor(ry / f32(2)))
+                v = prev[y, x]
+                return v[0] * f32(2), v[1] * f32(2)
+        u, geom = pyref.search_level(PX[l], PY[l], P1[l], ps, w, h, ps, st, it, norm, init, I0p=P0[l])
+        assert np.array_equal(u, us[l]), f"paper patch u differs at level {l}"
+        i0 = P0[l][ps:ps + h, ps:ps + w]
+        i1 = P1[l][ps:ps + h, ps:ps + w]
+        d = pyref.densify_paper(u, geom, i0, i1, w, h, ps, st)
+        assert np.array_equal(d, ds[l]), f"paper dense differs at level {l}"
+        prev = d
+    assert np.array_equal(out, ds[F])
+
+
+def test_paper_mode_identical_frames_give_zero_flow(oracle):
+    # with the template subtracted, identical frames give b = 0 exactly at u = 0
+    # (below 256 px, where Q8's ceil(x + 1e-5f) still samples the template's own
+    # pixels): zero flow everywhere -- unlike the reference (Q2)
+    I0, _ = shifted_pair(6, 64, 64)
+    flow = oracle.calc_u8(I0, I0, C=2, F=0, ps=8, it=8, overlap=0.5, paper=1)
+    assert np.array_equal(flow, np.zeros_like(flow))
+    assert np.abs(oracle.calc_u8(I0, I0, C=2, F=0, ps=8, it=8, overlap=0.5)).max() > 0.01
+
+
+def test_paper_mode_is_more_accurate_on_synthetic_pairs(oracle):
+    import disflow
+    e = {0: [], 1: []}
+    for seed in (0, 1, 2):
+        I0, I1, gt = disflow.synth_pair(seed, 320, 240, with_gt=True)
+        p = disflow.preset_params(disflow.Preset.MEDIUM, 320, 240)
+        for paper in e:
+            p.paper_mode = paper
+            f = oracle.calc_from_params(I0, I1, p)
+            e[paper].append(np.sqrt(((f - gt) ** 2).sum(-1)).mean())
+    assert np.mean(e[1]) < 0.85 * np.mean(e[0])
