@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -522,6 +524,9 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
 #ifndef DIS_STAGGER
 #define DIS_STAGGER 0  // measured: lockstep sub-batches 1-3% faster on 1080p MEDIUM (search dominates)
 #endif
+#ifndef DIS_SUB0_CALLER
+#define DIS_SUB0_CALLER 0  // 1: sub-batch 0 on the caller's stream (see run_batches)
+#endif
 #ifndef DIS_STAGE_MAJOR
 #define DIS_STAGE_MAJOR 1
 #endif
@@ -554,29 +559,70 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         c->last_batch = n;
         return DIS_OK;
     }
-    // sub-batch 0 runs on the caller's stream itself (no cross-queue hop
-    // between consecutive calls); 1..S-1 fork from it and join back into it
+    // Every sub-batch runs on a context-owned stream forked from and joined
+    // back into the caller's stream. (Running sub-batch 0 on the caller's stream
+    // saves a cross-queue hop, but HIP maps streams onto its few hardware
+    // queues in creation order, so whether the caller's stream shares a queue
+    // with sub[1] -- serialising the two sub-batches -- depended on how many
+    // streams the process had created before: 15k vs 20k pairs/s at 1080p.
+    // The context's own streams are created back to back, on distinct queues.)
+    const int k0 = DIS_SUB0_CALLER ? 1 : 0;
     DIS_HIP(hipEventRecord(c->fork, s));
-    for (int k = 1; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+    for (int k = k0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
     const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
     const bool stage_major = DIS_STAGE_MAJOR;
     for (size_t i = 0; i < stages.size() * S; ++i) {
         const int k = stage_major ? (int)(i % S) : (int)(i / stages.size());
         const int st = stage_major ? stages[i / S] : stages[i % stages.size()];
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
-        hipStream_t sk = k == 0 ? s : c->sub[k];
+        hipStream_t sk = k < k0 ? s : c->sub[k];
         dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
                                  stride, pair_stride, flow + (size_t)a * fpp, sk, st,
                                  (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
                                  DIS_STAGGER ? c->staged[k] : nullptr);
         if (r != DIS_OK) return r;
     }
-    for (int k = 1; k < S; ++k) {
+    for (int k = k0; k < S; ++k) {
         DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
         DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     }
     c->last_batch = n;
     return DIS_OK;
+}
+
+// Sub-batch streams: one pool per device for the whole process, created
+// back to back on first use and never destroyed. HIP maps each new stream
+// onto one of its few hardware queues (GPU_MAX_HW_QUEUES = 4) by usage at
+// creation time; streams created per context after earlier contexts were
+// destroyed landed two sub-batches on one queue (measured: every context
+// after the first ran 1080p MEDIUM at 16.5k instead of 20.5k pairs/s with
+// 2 streams; 20.2k with 1). Contexts on a device share the pool: work of
+// concurrent contexts is ordered within a shared stream, still correct.
+bool sub_streams(int device, hipStream_t (&out)[dis_ctx::kMaxSub])
+{
+    static std::mutex mu;
+    static std::map<int, std::vector<hipStream_t>> pools;
+    std::lock_guard<std::mutex> lock(mu);
+    auto& v = pools[device];
+    if (v.empty()) {
+        // pipelined sub-batches (DIS_STAGGER_PRIO): later sub-batches get the
+        // higher priority, so the workgroups of their latency-bound coarse
+        // levels are dispatched as soon as the earlier sub-batch's retire
+        int prio_lo = 0, prio_hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+        for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+            hipStream_t st = nullptr;
+            if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking,
+                                            (DIS_STAGGER_PRIO && k > 0) ? prio_hi : prio_lo) != hipSuccess) {
+                for (hipStream_t x : v) hipStreamDestroy(x);
+                v.clear();
+                return false;
+            }
+            v.push_back(st);
+        }
+    }
+    for (int k = 0; k < dis_ctx::kMaxSub; ++k) out[k] = v[k];
+    return true;
 }
 
 }  // namespace
@@ -725,15 +771,9 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
         c->vr_plane = (long long)g.lv[g.F].W * g.lv[g.F].H;  // the largest refined level
         ok = hipMalloc(&c->vr_ws, sizeof(float) * dis::kVarRefPlanes * c->vr_plane * B) == hipSuccess;
     }
-    // pipelined sub-batches: later sub-batches get the higher priority, so the
-    // workgroups of their latency-bound coarse levels are dispatched as soon
-    // as the earlier sub-batch's search workgroups retire (not after them)
-    int prio_lo = 0, prio_hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+    ok = ok && sub_streams(device, c->sub);
     for (int k = 0; ok && k < dis_ctx::kMaxSub; ++k)
-        ok = hipStreamCreateWithPriority(&c->sub[k], hipStreamNonBlocking,
-                                         (DIS_STAGGER_PRIO && k > 0) ? prio_hi : prio_lo) == hipSuccess &&
-             hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess &&
+        ok = hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->staged[k], hipEventDisableTiming) == hipSuccess;
     // The capture-only stream exists only under refinement and is created last:
     // HIP assigns streams to its (GPU_MAX_HW_QUEUES = 4) hardware queues round
@@ -745,7 +785,6 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
     if (!ok) {
         free_ws(c);
         for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
-            if (c->sub[k]) hipStreamDestroy(c->sub[k]);
             if (c->join[k]) hipEventDestroy(c->join[k]);
             if (c->staged[k]) hipEventDestroy(c->staged[k]);
         }
@@ -764,11 +803,11 @@ dis_status dis_destroy(dis_ctx* c)
     if (!c) return DIS_OK;
     hipSetDevice(c->device);
     if (c->own) hipStreamSynchronize(c->own);
+    for (int k = 0; k < dis_ctx::kMaxSub; ++k)  // the streams are shared (process pool): wait for this
+        if (c->join[k]) hipEventSynchronize(c->join[k]);  // context's last join, not the stream
     free_ws(c);
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
     for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
-        if (c->sub[k]) hipStreamSynchronize(c->sub[k]);
-        if (c->sub[k]) hipStreamDestroy(c->sub[k]);
         if (c->join[k]) hipEventDestroy(c->join[k]);
         if (c->staged[k]) hipEventDestroy(c->staged[k]);
     }

@@ -1,7 +1,4 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-L=optical-flow-using-dense-inverse-search_amd/disflow
-timeout -k 10 600 python3 tools/ab.py --spawn 2 --rounds 2 --steps 10 $L/libdis_hip.so:streams=2 $L/libdis_hip.so:streams=1 $L/libdis_hip.so:streams=3 > gpurun_out/ab.log 2>&1 || { tail gpurun_out/ab.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/ab.log
-timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_a.log 2>&1 || exit $?
-tail -1 gpurun_out/bench_a.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+timeout -k 10 200 python tools/ctx_probe.py 4 > gpurun_out/c.log 2>&1 || { tail gpurun_out/c.log; exit 1; }
+grep -v amdgpu gpurun_out/c.log

@@ -7,6 +7,7 @@ resident in HBM, batch per call as given, `steps` timed calls after warmup.
   config 2  1920x1080  MEDIUM            (as bench.py)
   config 3  3840x2160  MEDIUM
   config 5  3840x2160  SLOW + variational refinement (3 fixed-point iterations per level)
+  2p        1920x1080  MEDIUM in paper mode
   colour    1920x1080  Middlebury colour coding of 32 flow fields (dis_flow_color)
 """
 import argparse
@@ -27,12 +28,14 @@ CONFIGS = {
     "2": ("1920x1080 MEDIUM", 1920, 1080, "MEDIUM", 32),
     "3": ("3840x2160 MEDIUM", 3840, 2160, "MEDIUM", 8),
     "5": ("3840x2160 SLOW + variational refinement", 3840, 2160, "SLOW", 2),
+    "2p": ("1920x1080 MEDIUM paper mode", 1920, 1080, "MEDIUM", 32, 1),
 }
 
 
-def run(name, W, H, preset, B, steps, warmup):
+def run(name, W, H, preset, B, steps, warmup, paper=0):
     dev = torch.device("cuda", 0)
     p = disflow.preset_params(disflow.Preset[preset], W, H)
+    p.paper_mode = paper
     pairs = [disflow.synth_pair(k, W, H) for k in range(B)]
     d0 = torch.from_numpy(np.stack([a for a, _ in pairs])).to(dev)
     d1 = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
@@ -51,7 +54,8 @@ def run(name, W, H, preset, B, steps, warmup):
     eng.close()
     return {"config": name, "preset": preset, "knobs": {"C": p.coarsest_scale, "F": p.finest_scale,
                                                         "it": p.iterations, "overlap": p.patch_overlap,
-                                                        "var_refine_iters": p.var_refine_iters},
+                                                        "var_refine_iters": p.var_refine_iters,
+                                                        "paper_mode": p.paper_mode},
             "batch": B, "steps": steps, "ms_per_step": el / steps * 1e3, "pairs_per_s": B * steps / el,
             "patches_per_pair": wl["patches"], "updates_per_pair": wl["updates"],
             "updates_per_s": wl["updates"] * B * steps / el}
@@ -84,7 +88,7 @@ def run_colour(steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,2,3,5,colour")
+    ap.add_argument("--configs", default="1,2,3,5,2p,colour")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
@@ -92,9 +96,9 @@ def main():
         if c == "colour":
             r = run_colour(a.steps, a.warmup)
         else:
-            name, W, H, preset, B = CONFIGS[c]
+            name, W, H, preset, B = CONFIGS[c][:5]
             steps = max(2, a.steps // (4 if c == "5" else 1))
-            r = run(f"config {c}: {name}", W, H, preset, B, steps, a.warmup)
+            r = run(f"config {c}: {name}", W, H, preset, B, steps, a.warmup, *CONFIGS[c][5:])
         print(json.dumps(r), flush=True)
 
 
