@@ -51,6 +51,8 @@ def main():
             p.iterations = int(opts.pop("iters"))
         if "vr" in opts:
             p.var_refine_iters = int(opts.pop("vr"))
+        if "paper" in opts:
+            p.paper_mode = int(opts.pop("paper"))
         eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
         for k, val in opts.items():
             if k == "streams":
