@@ -40,10 +40,9 @@ __device__ __forceinline__ float bilinear_replicate(const float* __restrict__ I,
     const int xa = (int)fx0, ya = (int)fy0;
     const float fx = X - fx0, fy = Y - fy0;
     const int c0 = clampi(xa, 0, W - 1), c1 = clampi(xa + 1, 0, W - 1);
-    const float* r0 = I + (size_t)clampi(ya, 0, H - 1) * W;
-    const float* r1 = I + (size_t)clampi(ya + 1, 0, H - 1) * W;
-    const float top = (1.0f - fx) * r0[c0] + fx * r0[c1];
-    const float bot = (1.0f - fx) * r1[c0] + fx * r1[c1];
+    const unsigned o0 = (unsigned)(clampi(ya, 0, H - 1) * W), o1 = (unsigned)(clampi(ya + 1, 0, H - 1) * W);
+    const float top = (1.0f - fx) * I[o0 + c0] + fx * I[o0 + c1];  // 32-bit offsets: a plane < 2^31 floats
+    const float bot = (1.0f - fx) * I[o1 + c0] + fx * I[o1 + c1];
     return (1.0f - fy) * top + fy * bot;
 }
 

@@ -252,7 +252,7 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 //    121-182), 3) F == 0: crop; F >= 1: scale by 2^F, resize, crop.
 // K = ceil(ps / steps) bounds the covering patches per axis, so the gather is
 // an unrolled, predicated K x K loop (no divergent loops).
-template <bool UPSAMPLE, int K>
+template <bool UPSAMPLE, int K, bool kPaper = false>
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
     constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
@@ -297,10 +297,11 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const int cx = k / kOutPY, cy = k % kOutPY;
             v[j] = (cx < PW && cy < PH) ? u[(ga + cx) * a.nph + ha + cy] : make_float2(0.f, 0.f);
         }
-        // new_u = u * 0.5 (src/patch_grid.cpp:156), formed once per patch
+        // new_u = u * 0.5 (src/patch_grid.cpp:156), formed once per patch (paper mode: u itself)
 #pragma unroll
         for (int j = 0; j < NL; ++j)
-            if (tid + 256 * j < kOutPX * kOutPY) pu[tid + 256 * j] = make_float2(v[j].x * 0.5f, v[j].y * 0.5f);
+            if (tid + 256 * j < kOutPX * kOutPY)
+                pu[tid + 256 * j] = kPaper ? v[j] : make_float2(v[j].x * 0.5f, v[j].y * 0.5f);
     }
     // covering patch ranges per window column / row (one floordiv pair each)
     if (tid < rw) {
@@ -321,16 +322,38 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         // terms add +0, an exact no-op (f is never -0)
         const int2 xr = cr[c], yr = rr[r];
         float fx = 0.0f, fy = 0.0f, w = 0.0f;
+        if constexpr (kPaper) {
+            // SURVEY 8f row 4 (oracle densify_paper): weight 1/max(1, |I1(x+u) - I0(x)|)
+            const int xg = i0 + c, yg = j0 + r;  // level-F pixel
+            const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
+            const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
+            const float i0v = I0[(size_t)yg * a.wF + xg];
 #pragma unroll
-        for (int i = 0; i < K; ++i)
+            for (int i = 0; i < K; ++i)
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const bool ok = (xr.x + i <= xr.y) && (yr.x + j <= yr.y);
-                const float2 t = pu[ok ? (xr.x + i) * kOutPY + yr.x + j : 0];
-                fx = fx + (ok ? t.x : 0.0f);
-                fy = fy + (ok ? t.y : 0.0f);
-                w = w + (ok ? 0.5f : 0.0f);
-            }
+                for (int j = 0; j < K; ++j) {
+                    if ((xr.x + i <= xr.y) && (yr.x + j <= yr.y)) {
+                        const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
+                        const float d =
+                            bilinear_replicate(I1, a.wF, a.hF, (float)xg + t.x, (float)yg + t.y) - i0v;
+                        const float cw = 1.0f / fmaxf(1.0f, fabsf(d));
+                        fx = fx + cw * t.x;
+                        fy = fy + cw * t.y;
+                        w = w + cw;
+                    }
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const bool ok = (xr.x + i <= xr.y) && (yr.x + j <= yr.y);
+                    const float2 t = pu[ok ? (xr.x + i) * kOutPY + yr.x + j : 0];
+                    fx = fx + (ok ? t.x : 0.0f);
+                    fy = fy + (ok ? t.y : 0.0f);
+                    w = w + (ok ? 0.5f : 0.0f);
+                }
+        }
         if (w > 0) {
             fx = fx / w;
             fy = fy / w;
@@ -406,10 +429,16 @@ bool output_fits(const OutputArgs& a)
 template <int K>
 static void launch_output_k(const OutputArgs& a, dim3 grid, hipStream_t s, Timing t)
 {
-    if (a.F == 0)
+    if (a.paper) {
+        if (a.F == 0)
+            DIS_LAUNCH(t, (k_output<false, K, true>), grid, dim3(256), 0, s, a);
+        else
+            DIS_LAUNCH(t, (k_output<true, K, true>), grid, dim3(256), 0, s, a);
+    } else if (a.F == 0) {
         DIS_LAUNCH(t, (k_output<false, K>), grid, dim3(256), 0, s, a);
-    else
+    } else {
         DIS_LAUNCH(t, (k_output<true, K>), grid, dim3(256), 0, s, a);
+    }
 }
 
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t)

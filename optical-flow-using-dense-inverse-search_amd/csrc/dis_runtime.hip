@@ -268,6 +268,32 @@ int upsample_xmax(const dis::Geometry& g)
 
 constexpr int kStageFront = 1000, kStageBack = -1000;  // other stages: the level index
 
+// k_densify arguments for level l of a sub-batch's workspace slice
+dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const float* img1, float2* pu,
+                              float2* dense)
+{
+    const dis::Geometry& g = c->g;
+    const dis::LevelGeom& L = g.lv[l];
+    dis::DensifyArgs d{};
+    d.img0 = img0 + L.plane_off;
+    d.img1 = img1 + L.plane_off;
+    d.plane_stride = g.plane_stride;
+    d.paper = c->p.paper_mode != 0 ? 1 : 0;
+    d.u = pu + L.u_off;
+    d.dense = dense + L.dense_off;
+    d.u_stride = g.u_stride;
+    d.dense_stride = g.dense_stride;
+    d.W = L.W;
+    d.H = L.H;
+    d.ps = g.ps;
+    d.steps = L.steps;
+    d.npw = L.npw;
+    d.nph = L.nph;
+    d.offw = L.offw;
+    d.offh = L.offh;
+    return d;
+}
+
 // One stage of the path for n pairs already resident in device memory: the
 // front end (pyramid), one level (search, and densify + refinement when on),
 // or the back end (output). run_batches issues the stages stage-major across
@@ -289,9 +315,6 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     const bool fast = g.ps == 8 && c->variant != 1;
     const bool vr = c->p.var_refine_iters > 0;
     const bool paper = c->p.paper_mode != 0;
-    // every level's dense field is materialised (and seeds the next level) under
-    // refinement and in paper mode (weighted densification needs the images)
-    const bool dense_path = vr || paper;
     if (stage == kStageFront && wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
     if (stage == kStageFront) {
         if (fast && g.C >= 1) {
@@ -389,7 +412,34 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             b.fb_count = fb_count + l;
             b.fb_list = c->fb + c->fb_list_off[sub][l];
             b.paper = paper ? 1 : 0;
-            if (dense_path && l < g.C) {  // init from the coarser level's (refined / weighted) dense field
+            if (paper && !vr && l < g.C) {
+                // weighted initialisation per patch, into this level's (unused) dense slot
+                const dis::LevelGeom& Lc = g.lv[l + 1];
+                dis::PaperInitArgs pi{};
+                pi.u_coarse = pu + Lc.u_off;
+                pi.init = dense + L.dense_off;
+                pi.img0 = img0 + Lc.plane_off;
+                pi.img1 = img1 + Lc.plane_off;
+                pi.u_stride = g.u_stride;
+                pi.init_stride = g.dense_stride;
+                pi.plane_stride = g.plane_stride;
+                pi.npw = L.npw;
+                pi.nph = L.nph;
+                pi.offw = L.offw;
+                pi.offh = L.offh;
+                pi.steps = L.steps;
+                pi.c_npw = Lc.npw;
+                pi.c_nph = Lc.nph;
+                pi.c_offw = Lc.offw;
+                pi.c_offh = Lc.offh;
+                pi.c_W = Lc.W;
+                pi.c_H = Lc.H;
+                pi.hp = g.ps / 2;
+                DIS_HIP(dis::launch_paper_init(pi, n, s));
+                b.u_init = pi.init;
+                b.init_stride = pi.init_stride;
+            }
+            if (vr && l < g.C) {  // refined dense flows: init from the coarser level's dense field
                 b.dense_coarse = dense + g.lv[l + 1].dense_off;
                 b.dense_stride = g.dense_stride;
             }
@@ -399,25 +449,12 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         }
-        if (fast && !c->debug && !dense_path) continue;  // the fused output kernel densifies the finest level
-        dis::DensifyArgs d{};
-        d.img0 = img0 + L.plane_off;
-        d.img1 = img1 + L.plane_off;
-        d.plane_stride = g.plane_stride;
-        d.paper = paper ? 1 : 0;
-        d.u = pu + L.u_off;
-        d.dense = dense + L.dense_off;
-        d.u_stride = g.u_stride;
-        d.dense_stride = g.dense_stride;
-        d.W = L.W;
-        d.H = L.H;
-        d.ps = g.ps;
-        d.steps = L.steps;
-        d.npw = L.npw;
-        d.nph = L.nph;
-        d.offw = L.offw;
-        d.offh = L.offh;
-        DIS_HIP(dis::launch_densify(d, n, s));
+        // the fast path materialises dense fields only under refinement (the next
+        // level initialises from the refined field); otherwise the search fuses
+        // the coarser level's densification at its sampled pixels and the output
+        // kernel densifies the finest level
+        if (fast && !c->debug && !vr) continue;
+        DIS_HIP(dis::launch_densify(densify_args(c, l, img0, img1, pu, dense), n, s));
         if (vr) {  // variational refinement of the level's dense flow
             dis::VarRefArgs v{};
             v.img0 = img0 + L.plane_off;
@@ -479,28 +516,17 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         o.hp = g.ps / 2;
         o.vec_store = ((reinterpret_cast<uintptr_t>(flow) & 15) == 0 && (g.W & 1) == 0) ? 1 : 0;
         o.sc = std::pow(2.0f, (float)g.F);
-        fused_out = dis::output_fits(o) && !dense_path;  // refined / paper: the finest dense field exists
+        o.paper = paper ? 1 : 0;
+        o.img0 = img0 + LF.plane_off;
+        o.img1 = img1 + LF.plane_off;
+        o.plane_stride = g.plane_stride;
+        fused_out = dis::output_fits(o) && !vr;  // refined: the finest dense field exists
     }
     if (fused_out) {
         DIS_HIP(dis::launch_output(o, n, s, timing(c, 3)));
     } else {
-        if (fast && !c->debug && !dense_path) {  // the search loop skipped the finest densify: do it here
-            const dis::LevelGeom& L = g.lv[g.F];
-            dis::DensifyArgs d{};
-            d.u = pu + L.u_off;
-            d.dense = dense + L.dense_off;
-            d.u_stride = g.u_stride;
-            d.dense_stride = g.dense_stride;
-            d.W = L.W;
-            d.H = L.H;
-            d.ps = g.ps;
-            d.steps = L.steps;
-            d.npw = L.npw;
-            d.nph = L.nph;
-            d.offw = L.offw;
-            d.offh = L.offh;
-            DIS_HIP(dis::launch_densify(d, n, s));
-        }
+        if (fast && !c->debug && !vr)  // the level loop skipped the finest densify: do it here
+            DIS_HIP(dis::launch_densify(densify_args(c, g.F, img0, img1, pu, dense), n, s));
         const dis::LevelGeom& LF = g.lv[g.F];
         dis::UpsampleArgs u{};
         u.dense = dense + LF.dense_off;

@@ -398,7 +398,10 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int hp = 4;
     int ga = 0, ha = 0, PH = 0, PN = 0;
     float2 cuv[kCuPer<LPP>];
-    const float2* uc = (a.u_coarse && !a.dense_coarse) ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
+    const float2* uc =
+        (a.u_coarse && !a.dense_coarse && !a.u_init) ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
+    const float2 uinit = (a.u_init && active) ? a.u_init[(size_t)pair * a.init_stride + gx * a.nph + gy]
+                                              : make_float2(0.0f, 0.0f);
     if (uc) {
         const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
         const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
@@ -542,7 +545,10 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2,
     // gathered from the staged coarse displacements.
     float ix = 0.0f, iy = 0.0f;
-    if (a.dense_coarse && active) {
+    if (a.u_init && active) {  // paper mode: the weighted initialisation (k_paper_init), loaded in step 1
+        ix = uinit.x;
+        iy = uinit.y;
+    } else if (a.dense_coarse && active) {
         // from the coarser level's dense flow (refined): src/patch_grid.cpp:108-119
         const float2 d = a.dense_coarse[(size_t)pair * a.dense_stride + (size_t)(iry >> 1) * (W / 2) + (irx >> 1)];
         ix = d.x * 2;
