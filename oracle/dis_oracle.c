@@ -32,6 +32,37 @@
  * .sum() on the path: src/patch.cpp:82-84, 171-172, 265. */
 static float eigen_sum(const float* x, int n)
 {
+#if defined(DIS_ORACLE_SEQ_SUM)
+    /* tolerance calibration only: plain left-to-right order */
+    float q = x[0];
+    for (int i = 1; i < n; ++i) q = q + x[i];
+    return q;
+#elif defined(DIS_ORACLE_AVX_SUM)
+    /* tolerance calibration only: Eigen with 8-wide AVX packets
+     * (two packet accumulators over blocks of 16, predux = lo4 + hi4, then the
+     * 4-wide (q0+q2)+(q1+q3)) */
+    if (n >= 8) {
+        const int a8 = (n / 8) * 8, a16 = (n / 16) * 16;
+        float p0[8], p1[8];
+        for (int j = 0; j < 8; ++j) p0[j] = x[j];
+        if (a8 > 8) {
+            for (int j = 0; j < 8; ++j) p1[j] = x[8 + j];
+            for (int i = 16; i < a16; i += 16)
+                for (int j = 0; j < 8; ++j) {
+                    p0[j] = p0[j] + x[i + j];
+                    p1[j] = p1[j] + x[i + 8 + j];
+                }
+            for (int j = 0; j < 8; ++j) p0[j] = p0[j] + p1[j];
+            if (a8 > a16)
+                for (int j = 0; j < 8; ++j) p0[j] = p0[j] + x[a16 + j];
+        }
+        float h[4];
+        for (int j = 0; j < 4; ++j) h[j] = p0[j] + p0[4 + j];
+        float r = (h[0] + h[2]) + (h[1] + h[3]);
+        for (int i = a8; i < n; ++i) r = r + x[i];
+        return r;
+    }
+#endif
     if (n < 4) { /* DefaultTraversal */
         float r = x[0];
         for (int i = 1; i < n; ++i) r = r + x[i];
