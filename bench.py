@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU-baseline host processes (0 = all, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="process group backend for N > 1 (nccl = RCCL; "
+                    "gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch events")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per search launch (from tools/pmc_traffic.py)")
@@ -125,11 +127,15 @@ def main():
                          f"C oracle (oracle/dis_oracle.c, gcc -O2 -ffp-contract=off)",
                "single_core": {"value": c["single_core"]["value"], "pairs": c["single_core"]["pairs"],
                                "cores": 1}}
+    local = local % max(1, torch.cuda.device_count())  # ranks > GPUs only in a one-GPU rehearsal
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     def barrier():
         if world > 1:
@@ -178,7 +184,24 @@ def main():
         n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
         eng.set_kernel_timing(False)
         eng.set_concurrency(a.streams if a.streams else 2)
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    # the path's one collective, outside the timed region: the
+    # last step's flows of every rank gathered to rank 0 over RCCL/xGMI
+    gather = None
+    if world > 1:
+        import disflow.multi as multi
+        barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        full = multi.gather_flow_tensor(out, world * B, rank, world)
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter() - tg
+        if rank == 0:
+            nbytes = (world - 1) * out.numel() * out.element_size()  # bytes that crossed xGMI
+            gather = {"ms": tg * 1e3, "bytes_received": nbytes, "GB_per_s": nbytes / tg / 1e9,
+                      "pairs": int(full.shape[0]),
+                      "backend": "nccl (RCCL)" if a.dist_backend == "nccl" else a.dist_backend}
+            del full
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
     el = float(el_t.item())
@@ -246,6 +269,7 @@ def main():
                                  "launch of that kernel (profiles/traffic.json)"},
             "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
             "cpu_baseline": cpu,
+            "gather": gather,
             "max_epe_vs_oracle": max_epe,
         }
         print(json.dumps(line), flush=True)

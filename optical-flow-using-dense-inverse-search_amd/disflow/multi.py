@@ -78,3 +78,34 @@ def run_sharded(I0: np.ndarray, I1: np.ndarray, params, width: int, height: int,
     if gather_flows:
         out["flows"] = np.concatenate([p["flows"] for p in parts])
     return out
+
+
+def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
+    """The single collective of the multi-GPU path: gather every
+    rank's (n_r, H, W, 2) float32 flows -- device tensors under RCCL (`nccl`),
+    host tensors under gloo -- into one (n_total, H, W, 2) tensor on rank 0,
+    in pair order (shard_bounds blocks). Shards may differ by one pair: each is
+    padded to the largest before the gather and cut after. Returns the tensor on
+    rank 0 and None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "gloo" and local.is_cuda:  # gloo gathers host tensors
+        local = local.cpu()
+    a, b = shard_bounds(n_total, rank, world)
+    if local.shape[0] != b - a:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} flows, its shard is {b - a}")
+    m = max(shard_bounds(n_total, r, world)[1] - shard_bounds(n_total, r, world)[0] for r in range(world))
+    send = local
+    if local.shape[0] < m:
+        send = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        send[:local.shape[0]] = local
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    dist.gather(send.contiguous(), recv, dst=0, group=group)
+    if rank != 0:
+        return None
+    parts = []
+    for r in range(world):
+        ra, rb = shard_bounds(n_total, r, world)
+        parts.append(recv[r][:rb - ra])
+    return torch.cat(parts)

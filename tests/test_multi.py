@@ -64,6 +64,26 @@ def _worker(rank, world, port, n, out_q, use_gpu):
         dist.destroy_process_group()
 
 
+def _gather_worker(rank, world, port, n, out_q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        I0, I1 = _pairs(n)
+        a, b = multi.shard_bounds(n, rank, world)
+        local = torch.from_numpy(_fake_compute(I0[a:b], I1[a:b]))
+        got = multi.gather_flow_tensor(local, n, rank, world)
+        if rank == 0:
+            out_q.put(got.numpy())
+        else:
+            assert got is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def _gpu_pairs(n):
     import disflow
     pairs = [disflow.synth_pair(100 + k, 192, 144) for k in range(n)]
@@ -104,3 +124,21 @@ def test_two_ranks_on_one_gpu_match_single_process():
     single = multi.run_sharded(I0, I1, p, W, H, max_batch=6, gather_flows=True)
     assert digests == single["digests"]
     assert np.array_equal(flows.view(np.uint32), single["flows"].view(np.uint32))
+
+
+@pytest.mark.parametrize("world,n", [(2, 7), (3, 8)])
+def test_gloo_tensor_gather_uneven_shards(world, n):
+    # the bench's RCCL gather (gather_flow_tensor) with gloo on CPU tensors:
+    # shards of unequal size come back whole and in pair order
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    I0, I1 = _pairs(n)
+    assert np.array_equal(got, _fake_compute(I0, I1))
