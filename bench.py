@@ -67,10 +67,31 @@ def make_pairs(seeds, W, H):
     return np.stack([a for a, _ in res]), np.stack([b for _, b in res])
 
 
+CPU_WORKER_CAP = 16  # the GPU box's CPU share per GPU (gpurun: 16); nproc shows the whole host
+
+
+def oracle_lib_for_baseline():
+    """The -O3 build of the oracle (the CPU baseline is the C
+    restatement at -O3, single-threaded per pair); -O2 checker build otherwise."""
+    o3 = os.path.join(ROOT, "oracle", "libdis_oracle_o3.so")
+    return o3 if os.path.exists(o3) else os.path.join(ROOT, "oracle", "libdis_oracle.so")
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def _cpu_worker(args):
     """One host process of the CPU baseline: oracle pairs until the deadline."""
     k0, step, W, H, pfields, deadline = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["DIS_ORACLE_LIB"] = oracle_lib_for_baseline()
     import oracle_binding
 
     params = disflow.Params(**pfields)
@@ -108,26 +129,73 @@ def cpu_baseline(params, W, H, budget_s, workers):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """`--gpus N > 1` without a launcher: start the N ranks ourselves as
+    `torch.distributed.run` children (one process per GPU, rendezvous on
+    127.0.0.1) and exit with their status. Runs before anything touches the
+    GPU (this process only counts devices), so nothing is re-exec'd."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: --gpus {a.gpus} without WORLD_SIZE: launching {a.gpus} ranks under torch.distributed.run",
+          file=sys.stderr, flush=True)
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+def check_world(a, world, rank):
+    """The line must describe the ranks that really ran: --gpus == WORLD_SIZE,
+    and under nccl (RCCL) one distinct GPU per local rank."""
+    if a.gpus != world:
+        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE {world}: refusing to report a "
+                         f"{world}-rank measurement as {a.gpus} GPUs")
+    if a.dist_backend == "nccl" and world > 1:
+        ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if lws > ndev:
+            raise SystemExit(f"bench: {lws} local ranks but {ndev} visible GPU(s) under nccl: ranks would "
+                             f"share a GPU (use --dist-backend gloo only to rehearse that)")
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    check_world(a, world, rank)
+    if os.environ.get("DIS_BENCH_PLAN_ONLY"):  # tests: the rank layout, before any GPU call
+        print(json.dumps({"rank": rank, "world": world, "gpus": a.gpus, "backend": a.dist_backend}), flush=True)
+        return
     W, H, B = a.width, a.height, a.batch
     params = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # before any GPU call (plain forks)
-        workers = a.cpu_workers or min(16, len(os.sched_getaffinity(0)))
+        affinity = len(os.sched_getaffinity(0))
+        workers = a.cpu_workers or min(CPU_WORKER_CAP, affinity)
         c = cpu_baseline(params, W, H, a.cpu_seconds, workers)
+        lib = os.path.basename(oracle_lib_for_baseline())
         cpu = {"value": c["value"], "unit": "frame-pairs/s", "cores": c["cores"], "kind": "port",
                "sample": f"{c['pairs']} synthetic {W}x{H} pairs, preset={a.preset}, in {c['cores']} host "
                          f"processes (one pair at a time each, like the reference) for {2 * a.cpu_seconds / 3:.0f} s; "
-                         f"C oracle (oracle/dis_oracle.c, gcc -O2 -ffp-contract=off)",
+                         f"C oracle (oracle/dis_oracle.c as {lib}, gcc -O3 -ffp-contract=off)",
+               "host": {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": cpu_model(),
+                        "worker_cap": CPU_WORKER_CAP,
+                        "note": f"workers = min({CPU_WORKER_CAP}, CPUs in this process's affinity mask): "
+                                "the cap is a choice (the GPU box grants one GPU's share of the host, "
+                                "16 CPUs, although nproc shows the whole machine)"},
                "single_core": {"value": c["single_core"]["value"], "pairs": c["single_core"]["pairs"],
                                "cores": 1}}
-    local = local % max(1, torch.cuda.device_count())  # ranks > GPUs only in a one-GPU rehearsal
+    if a.dist_backend != "nccl":  # gloo rehearsal: several ranks may share one GPU
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -176,8 +244,7 @@ def main():
     if not a.no_kernel_timing:
         eng.set_concurrency(1)
         step()
-        eng.set_kernel_timing(True)
-        eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)  # reset accumulated records
+        eng.set_kernel_timing(True)  # (re)enabling starts a fresh measurement
         for _ in range(max(3, a.steps // 5)):
             step()
         torch.cuda.synchronize(dev)
@@ -195,10 +262,20 @@ def main():
         full = multi.gather_flow_tensor(out, world * B, rank, world)
         torch.cuda.synchronize(dev)
         tg = time.perf_counter() - tg
+        # verify the collective: every rank's bit-level checksum of its own
+        # shard against rank 0's checksum of that shard of the gathered tensor
+        sums = multi.gather_checksums(multi.flow_checksum(out), rank, world)
         if rank == 0:
+            if int(full.shape[0]) != world * B:
+                raise SystemExit(f"bench: gathered {full.shape[0]} pairs, expected {world * B}")
+            got = [multi.flow_checksum(full[r * B:(r + 1) * B]) for r in range(world)]
+            verified = all(torch.equal(g.cpu(), e.cpu()) for g, e in zip(got, sums))
+            if not verified:
+                raise SystemExit("bench: gathered flows differ from the ranks' own flows")
             nbytes = (world - 1) * out.numel() * out.element_size()  # bytes that crossed xGMI
             gather = {"ms": tg * 1e3, "bytes_received": nbytes, "GB_per_s": nbytes / tg / 1e9,
-                      "pairs": int(full.shape[0]),
+                      "pairs": int(full.shape[0]), "verified": verified,
+                      "world_size": torch.distributed.get_world_size(),
                       "backend": "nccl (RCCL)" if a.dist_backend == "nccl" else a.dist_backend}
             del full
     el_t = torch.tensor([el], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")

@@ -5,7 +5,7 @@
 //                             (the per-pair body of src/main.cpp:135-198)
 //   OpticalFlow::OpticalFlowClass
 //                             drop-in for the reference constructor with the
-//                             identical signature (include/optical_flow.hpp:53-64,
+//                             identical signature (include/optical_flow.hpp:43-54,
 //                             src/optical_flow.cpp:19-91): padded host pyramids
 //                             in, finest-level flow out, computed on the GPU.
 //
@@ -141,7 +141,7 @@ inline std::vector<float> read_flo(const std::string& path, int* width, int* hei
 namespace OpticalFlow {
 
 // Same constructor signature and semantics as the reference
-// (include/optical_flow.hpp:53-64): the whole coarse-to-fine computation runs
+// (include/optical_flow.hpp:43-54): the whole coarse-to-fine computation runs
 // inside the constructor and writes `outflow` ((width>>F) x (height>>F) x 2).
 // draw_grid (an OpenCV GUI debug view) is not supported.
 class OpticalFlowClass {

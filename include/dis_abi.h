@@ -5,7 +5,7 @@
  * The reference (nejcgalof/Optical-Flow-using-Dense-Inverse-Search) has no
  * C-ABI or plugin interface; its hot path is reached through
  *   (R1) construct_pyramide()                       src/main.cpp:12-50
- *   (R2) OpticalFlow::OpticalFlowClass::ctor(...)   include/optical_flow.hpp:53-64,
+ *   (R2) OpticalFlow::OpticalFlowClass::ctor(...)   include/optical_flow.hpp:43-54,
  *                                                   src/optical_flow.cpp:19-91
  *   (R3) the pad / convert / upsample / crop glue   src/main.cpp:135-160, 191-198
  * Each entry point below names the reference interface it replaces. The C++
@@ -119,7 +119,7 @@ dis_status dis_calc_batch_u8(dis_ctx* ctx, int n, const uint8_t* I0, const uint8
                              dis_mem where, void* stream);
 
 /* Compatibility entry with the exact semantics of the reference constructor
- * OpticalFlowClass(...) (include/optical_flow.hpp:53-64): host pyramids of
+ * OpticalFlowClass(...) (include/optical_flow.hpp:43-54): host pyramids of
  * (coarsest+1) PADDED planes (row stride W_l + 2*img_padding, pointer at the
  * padded origin, as built by construct_pyramide, src/main.cpp:41-49), output
  * `outflow` = (width>>F) x (height>>F) x 2 floats at the finest level.
@@ -166,7 +166,11 @@ dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* d
 /* Per-kernel timing with HIP events recorded on the context's launch stream
  * around every launch of the named kernel class (bench / roofline use).
  * kernel: 0 = fused pyramid, 1 = patch search (all levels), 2 = patch search
- * (finest level only), 3 = fused densify+upsample+crop. */
+ * (finest level only), 3 = fused densify+upsample+crop. Enabling timing while
+ * it is off starts a fresh measurement (accumulated launches and times are
+ * cleared); dis_kernel_time returns the totals since then (the event pool
+ * grows as needed, so no launch is left out; DIS_ERR_DEVICE if event creation
+ * failed and records were lost). */
 dis_status dis_set_kernel_timing(dis_ctx* ctx, int enable);
 dis_status dis_kernel_time(dis_ctx* ctx, int kernel, int* launches, double* total_ms);
 

@@ -14,7 +14,7 @@ namespace dis {
 
 constexpr int kMaxLevels = 16;
 
-// One pyramid level of one pair (image_parameters, include/optical_flow.hpp:24-34,
+// One pyramid level of one pair (image_parameters, include/optical_flow.hpp:14-24,
 // plus the PatchGrid geometry, src/patch_grid.cpp:20-23).
 struct LevelGeom {
     int W, H;                      // level size (int(W*2^-l), src/optical_flow.cpp:51-53)

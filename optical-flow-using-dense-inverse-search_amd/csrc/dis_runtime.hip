@@ -58,7 +58,7 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
     g->Hp = H + padh;
     g->pad_left = padw / 2;
     g->pad_top = padh / 2;
-    // src/optical_flow.cpp:490
+    // src/optical_flow.cpp:38
     const int st = (int)std::floor((float)p.patch_size * (1.0f - p.patch_overlap));
     g->steps = st < 1 ? 1 : st;
     long long poff = 0, uoff = 0, doff = 0;
@@ -136,6 +136,11 @@ struct dis_ctx {
     int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
     hipStream_t sub[kMaxSub] = {};
     hipEvent_t fork = nullptr;
+    // end of the previous call's work on its stream: every call first orders
+    // its stream after it, so calls on different streams (calc_device on a
+    // caller stream, then calc_batch on `own`) never overlap on the workspace
+    hipEvent_t done = nullptr;
+    bool done_pending = false;
     hipEvent_t join[kMaxSub] = {};
     hipEvent_t staged[kMaxSub] = {};  // sub-batch k's pyramid done (pipelined start of k+1)
     // variational refinement: its ~16 launches per fixed-point iteration per level
@@ -174,6 +179,7 @@ struct dis_ctx {
     size_t pool_next = 0;
     int launches[4] = {0, 0, 0, 0};
     double total_ms[4] = {0, 0, 0, 0};
+    long long dropped = 0;  // records lost to a failed event creation (dis_kernel_time fails then)
 };
 
 namespace {
@@ -229,7 +235,17 @@ void free_ws(dis_ctx* c)
 dis::Timing timing(dis_ctx* c, int kind, int kind2 = -1)
 {
     dis::Timing t;
-    if (!c->timing || c->pool_next + 2 > c->pool.size()) return t;
+    if (!c->timing) return t;
+    if (c->pool_next + 2 > c->pool.size()) {  // grow: a record is never dropped
+        const size_t n0 = c->pool.size();
+        c->pool.resize(n0 + 1024);
+        for (size_t i = n0; i < c->pool.size(); ++i)
+            if (hipEventCreate(&c->pool[i]) != hipSuccess) {
+                c->pool.resize(i);
+                c->dropped += 1;
+                return t;
+            }
+    }
     t.start = c->pool[c->pool_next++];
     t.stop = c->pool[c->pool_next++];
     c->recs.push_back({kind, t.start, t.stop});
@@ -577,12 +593,15 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     std::vector<int> stages = {kStageFront};
     for (int l = c->g.C; l >= c->g.F; --l) stages.push_back(l);
     stages.push_back(kStageBack);
+    if (c->done_pending) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     if (S <= 1) {
         for (int st : stages) {
             dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
             if (r != DIS_OK) return r;
         }
         c->last_batch = n;
+        DIS_HIP(hipEventRecord(c->done, s));
+        c->done_pending = true;
         return DIS_OK;
     }
     // Every sub-batch runs on a context-owned stream forked from and joined
@@ -613,6 +632,8 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     }
     c->last_batch = n;
+    DIS_HIP(hipEventRecord(c->done, s));
+    c->done_pending = true;
     return DIS_OK;
 }
 
@@ -782,7 +803,8 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->in1, (size_t)width * height * B) == hipSuccess &&
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess;
     if (ok) {
         size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
         for (int k = 0; k < dis_ctx::kMaxSub; ++k)
@@ -815,6 +837,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
             if (c->staged[k]) hipEventDestroy(c->staged[k]);
         }
         if (c->fork) hipEventDestroy(c->fork);
+        if (c->done) hipEventDestroy(c->done);
         if (c->cap) hipStreamDestroy(c->cap);
         if (c->own) hipStreamDestroy(c->own);
         delete c;
@@ -829,6 +852,7 @@ dis_status dis_destroy(dis_ctx* c)
     if (!c) return DIS_OK;
     hipSetDevice(c->device);
     if (c->own) hipStreamSynchronize(c->own);
+    if (c->done_pending) hipEventSynchronize(c->done);  // the last call, on whatever stream it ran
     for (int k = 0; k < dis_ctx::kMaxSub; ++k)  // the streams are shared (process pool): wait for this
         if (c->join[k]) hipEventSynchronize(c->join[k]);  // context's last join, not the stream
     free_ws(c);
@@ -838,6 +862,7 @@ dis_status dis_destroy(dis_ctx* c)
         if (c->staged[k]) hipEventDestroy(c->staged[k]);
     }
     if (c->fork) hipEventDestroy(c->fork);
+    if (c->done) hipEventDestroy(c->done);
     for (auto& row : c->vrg)
         for (auto& G : row)
             if (G.exec) hipGraphExecDestroy(G.exec);
@@ -961,6 +986,16 @@ dis_status dis_set_kernel_timing(dis_ctx* c, int enable)
         c->pool.resize(8192);
         for (auto& e : c->pool) DIS_HIP(hipEventCreate(&e));
     }
+    if (enable && !c->timing) {  // (re)enabling starts a fresh measurement
+        for (auto& r : c->recs) DIS_HIP(hipEventSynchronize(r.b));
+        c->recs.clear();
+        c->pool_next = 0;
+        for (int k = 0; k < 4; ++k) {
+            c->launches[k] = 0;
+            c->total_ms[k] = 0.0;
+        }
+        c->dropped = 0;
+    }
     c->timing = enable ? 1 : 0;
     return DIS_OK;
 }
@@ -980,6 +1015,7 @@ dis_status dis_kernel_time(dis_ctx* c, int kernel, int* launches, double* total_
     }
     c->recs.clear();
     c->pool_next = 0;
+    if (c->dropped) return fail(DIS_ERR_DEVICE, "kernel timing records were dropped (event creation failed)");
     if (launches) *launches = c->launches[kernel];
     if (total_ms) *total_ms = c->total_ms[kernel];
     return DIS_OK;

@@ -339,7 +339,12 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
             py > a.tmp_ub_h) {
             u0 = ix;
             u1 = iy;
+#ifdef DIS_EXP_FULLITERS  // experiment: reset and keep iterating (fixed work per patch)
+            px = sx;
+            py = sy;
+#else
             break;
+#endif
         }
         if (counter > a.iters) break;
     }
@@ -631,7 +636,11 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
             iterate<LPP, false, kPaper>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
+#ifdef DIS_EXP_TAPBANKS  // experiment: lane-fixed, conflict-free tap addresses (wrong values)
+                const float* base = tile + (lane & 31) + ((w.X & 1) << 5) + 0 * qb;
+#else
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
+#endif
                 return [base, TS](int k, int c) { return base[k * TS + c]; };
             });
         }

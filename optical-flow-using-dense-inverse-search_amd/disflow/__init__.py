@@ -7,7 +7,7 @@ drive it. The interface mirrors the reference's entry points:
 * :class:`DenseInverseSearch` ``.calc(I0, I1)`` -- u8 frames to full-resolution
   flow (the reference's per-pair body, src/main.cpp:135-198);
 * :func:`optical_flow_from_pyramids` -- the ``OpticalFlow::OpticalFlowClass``
-  constructor (include/optical_flow.hpp:53-64) over caller-built padded
+  constructor (include/optical_flow.hpp:43-54) over caller-built padded
   pyramids, returning the finest-level flow;
 * :class:`Preset` -- build-defined presets.
 
@@ -306,7 +306,7 @@ def optical_flow_from_pyramids(img_first, img_first_dx, img_first_dy, img_second
                                iterations: int, patch_size: int, patch_overlap: float,
                                patch_normalization: bool, img_second_dx=None, img_second_dy=None,
                                device: int = 0) -> np.ndarray:
-    """OpticalFlowClass(...) (include/optical_flow.hpp:53-64) over padded host
+    """OpticalFlowClass(...) (include/optical_flow.hpp:43-54) over padded host
     pyramids (lists of float32 2-D arrays, level 0..C). Returns the finest-level
     flow ((height>>F) x (width>>F) x 2)."""
     nl = coarsest_scale + 1

@@ -44,6 +44,31 @@ def _default_compute(params, width: int, height: int, device: int, max_batch: in
     return compute
 
 
+class ShardFailure(RuntimeError):
+    """Raised on every rank of run_sharded when any rank's compute failed."""
+
+
+def _agree_or_fail(err, rank: int, world: int, group=None):
+    """Collective status check before the gather: each rank contributes 1 if
+    its compute raised; when any did, every rank raises ShardFailure at once
+    (instead of the healthy ranks blocking in the gather until the process
+    group times out). The failing rank re-raises its own exception."""
+    import torch
+    import torch.distributed as dist
+
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    flags = torch.zeros(world, dtype=torch.int32, device=dev)
+    flags[rank] = 0 if err is None else 1
+    dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+    bad = [r for r in range(world) if int(flags[r]) != 0]
+    if err is not None:
+        raise ShardFailure(f"rank {rank}: shard compute failed: {err!r}") from err
+    if bad:
+        raise ShardFailure(f"rank {rank}: rank(s) {bad} failed their shard; aborting")
+
+
 def run_sharded(I0: np.ndarray, I1: np.ndarray, params, width: int, height: int, *, rank: int = 0,
                 world: int = 1, device: int = 0, max_batch: int = 32, gather_flows: bool = False,
                 compute: Optional[Callable[[np.ndarray, np.ndarray], np.ndarray]] = None,
@@ -57,9 +82,17 @@ def run_sharded(I0: np.ndarray, I1: np.ndarray, params, width: int, height: int,
     """
     n = I0.shape[0]
     a, b = shard_bounds(n, rank, world)
-    if compute is None:
-        compute = _default_compute(params, width, height, device, max_batch)
-    local = compute(I0[a:b], I1[a:b]) if b > a else np.empty((0, height, width, 2), np.float32)
+    err = None
+    try:
+        if compute is None:
+            compute = _default_compute(params, width, height, device, max_batch)
+        local = compute(I0[a:b], I1[a:b]) if b > a else np.empty((0, height, width, 2), np.float32)
+    except Exception as e:  # noqa: BLE001 -- reported to every rank below, then re-raised
+        err = e
+    if world > 1:
+        _agree_or_fail(err, rank, world, group)
+    elif err is not None:
+        raise err
     digests = [flow_digest(f) for f in local]
     result = {"start": a, "stop": b, "digests": digests}
     if gather_flows:
@@ -100,12 +133,40 @@ def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
     if local.shape[0] < m:
         send = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         send[:local.shape[0]] = local
-    recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    # rank 0 receives straight into one (world, m, ...) buffer: with equal
+    # shards (the bench case) that buffer IS the result, no second copy
+    buf = torch.empty((world,) + tuple(send.shape), dtype=send.dtype, device=send.device) if rank == 0 else None
+    recv = list(buf.unbind(0)) if rank == 0 else None
     dist.gather(send.contiguous(), recv, dst=0, group=group)
     if rank != 0:
         return None
+    if all(shard_bounds(n_total, r, world)[1] - shard_bounds(n_total, r, world)[0] == m for r in range(world)):
+        return buf.view((world * m,) + tuple(send.shape[1:]))
     parts = []
     for r in range(world):
         ra, rb = shard_bounds(n_total, r, world)
-        parts.append(recv[r][:rb - ra])
+        parts.append(buf[r, :rb - ra])
     return torch.cat(parts)
+
+
+def flow_checksum(flows):
+    """Bit-level fingerprint of a float32 flow tensor, computed where it lives:
+    two int64 sums of its 32-bit patterns (plain and position-weighted,
+    wrapping), so a reordered, truncated or altered shard changes it."""
+    import torch
+
+    v = flows.contiguous().view(torch.int32).reshape(-1).to(torch.int64)
+    w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([v.sum(), (v * w).sum(), torch.tensor(v.numel(), device=v.device)])
+
+
+def gather_checksums(local_sum, rank: int, world: int, group=None):
+    """Every rank's flow_checksum to rank 0 (a list in rank order there, None
+    elsewhere)."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "gloo" and local_sum.is_cuda:
+        local_sum = local_sum.cpu()
+    recv = [local_sum.new_empty(local_sum.shape) for _ in range(world)] if rank == 0 else None
+    dist.gather(local_sum.contiguous(), recv, dst=0, group=group)
+    return recv

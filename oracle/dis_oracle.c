@@ -239,7 +239,7 @@ void dis_oracle_pyramid(const float* img, int Wp, int Hp, int coarsest,
 
 int dis_oracle_steps(int patch_size, float patch_overlap)
 {
-    /* src/optical_flow.cpp:490: max(1, (int)floor(ps*(1 - overlap))) in float */
+    /* src/optical_flow.cpp:38: max(1, (int)floor(ps*(1 - overlap))) in float */
     float f = floorf((float)patch_size * (1.0f - patch_overlap));
     int s = (int)f;
     return s < 1 ? 1 : s;
@@ -260,10 +260,10 @@ void dis_oracle_grid(int width_l, int height_l, int steps,
 /* ------------------------------------------------------------------------- */
 
 typedef struct {
-    /* fix_parameters (include/optical_flow.hpp:36-47) */
+    /* fix_parameters (include/optical_flow.hpp:26-37) */
     int ps, iterations, normalization, npts;
     float outlierthresh;
-    /* image_parameters (include/optical_flow.hpp:24-34) */
+    /* image_parameters (include/optical_flow.hpp:14-24) */
     int width, height, pad, tmp_w;
     float tmp_lb, tmp_ub_w, tmp_ub_h;
     /* SURVEY 8f row 4 (not in the reference): DIS-paper residual */

@@ -25,17 +25,17 @@ extern "C" {
 #endif
 
 typedef struct {
-    int coarsest_scale;      /* include/optical_flow.hpp:39 */
-    int finest_scale;        /* include/optical_flow.hpp:40 */
-    int patch_size;          /* include/optical_flow.hpp:41 */
-    int iterations;          /* include/optical_flow.hpp:42 */
-    float patch_overlap;     /* src/optical_flow.cpp:490 */
-    int patch_normalization; /* include/optical_flow.hpp:43 */
+    int coarsest_scale;      /* include/optical_flow.hpp:49 */
+    int finest_scale;        /* include/optical_flow.hpp:49 */
+    int patch_size;          /* include/optical_flow.hpp:51 */
+    int iterations;          /* include/optical_flow.hpp:50 */
+    float patch_overlap;     /* include/optical_flow.hpp:52, used at src/optical_flow.cpp:38 */
+    int patch_normalization; /* include/optical_flow.hpp:53 */
     int var_refine_iters;    /* 0 = the reference (no refinement) */
     int paper_mode;          /* 0 = the reference; 1 = DIS-paper residual + weighted densify */
 } dis_oracle_params;
 
-/* Grid geometry of one level (src/optical_flow.cpp:490, src/patch_grid.cpp:20-23). */
+/* Grid geometry of one level (src/optical_flow.cpp:38, src/patch_grid.cpp:20-23). */
 int dis_oracle_steps(int patch_size, float patch_overlap);
 void dis_oracle_grid(int width_l, int height_l, int steps,
                      int* npw, int* nph, int* offw, int* offh);

@@ -11,7 +11,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-LIB = os.path.join(ORACLE_DIR, "libdis_oracle.so")
+# DIS_ORACLE_LIB selects another build of the same source (bench.py's CPU
+# baseline uses the -O3 build libdis_oracle_o3.so)
+LIB = os.environ.get("DIS_ORACLE_LIB") or os.path.join(ORACLE_DIR, "libdis_oracle.so")
 
 
 class Params(ctypes.Structure):
@@ -29,7 +31,7 @@ class Params(ctypes.Structure):
 
 def _load():
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ORACLE_DIR, "dis_oracle.c")):
-        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR, "all", "o3"])
     L = ctypes.CDLL(LIB)
     I, F, V, Z = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
     P = ctypes.POINTER

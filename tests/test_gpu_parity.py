@@ -138,6 +138,32 @@ def test_device_resident_path(disflow_mod):
     assert np.array_equal(o[1].view(np.uint32), host.view(np.uint32))
 
 
+def test_calls_on_different_streams_do_not_race(disflow_mod):
+    # a one-pair call runs on the caller's stream without the
+    # fork/join events; the next call on another stream (host mode runs on the
+    # context's own stream) must still wait for it before reusing the workspace
+    import torch
+    W, H = 1280, 720
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    X0, X1 = disflow_mod.synth_pair(31, W, H)
+    Y0, Y1 = disflow_mod.synth_pair(32, W, H)
+    ref = disflow_mod.DenseInverseSearch(p, W, H, max_batch=1)
+    ex, ey = ref.calc(X0, X1), ref.calc(Y0, Y1)
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2)
+    d0 = torch.from_numpy(X0[None]).cuda()
+    d1 = torch.from_numpy(X1[None]).cuda()
+    out = torch.empty((1, H, W, 2), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        out.zero_()
+        eng.calc_device(1, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), side.cuda_stream)
+        gy = eng.calc(Y0, Y1)  # no synchronisation in between
+        side.synchronize()
+        assert np.array_equal(out[0].cpu().numpy().view(np.uint32), ex.view(np.uint32))
+        assert np.array_equal(gy.view(np.uint32), ey.view(np.uint32))
+
+
 def test_medium_1080p_full_size_bitexact(disflow_mod, oracle):
     # BASELINE config 2 workload at full size against the oracle (a few seconds on CPU)
     W, H = 1920, 1080

@@ -142,3 +142,95 @@ def test_gloo_tensor_gather_uneven_shards(world, n):
         assert p.exitcode == 0
     I0, I1 = _pairs(n)
     assert np.array_equal(got, _fake_compute(I0, I1))
+
+
+def _fail_worker(rank, world, port, bad_rank, out_q):
+    # one rank's compute raises: every rank must leave run_sharded promptly
+    # with ShardFailure (no wait for the process-group timeout)
+    import time
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=300))
+
+    def compute(I0, I1):
+        if rank == bad_rank:
+            raise ValueError("injected failure")
+        return _fake_compute(I0, I1)
+
+    t0 = time.time()
+    try:
+        I0, I1 = _pairs(6)
+        multi.run_sharded(I0, I1, None, 16, 12, rank=rank, world=world, compute=compute, gather_flows=True)
+        out_q.put((rank, "no error", time.time() - t0))
+    except multi.ShardFailure as e:
+        out_q.put((rank, str(e), time.time() - t0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (3, 0)])
+def test_gloo_failing_rank_fails_every_rank_promptly(world, bad):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, bad, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, msg, secs in res:
+        assert msg != "no error"
+        assert secs < 60  # far below the 300 s process-group timeout
+        if rank == bad:
+            assert "injected failure" in msg
+        else:
+            assert f"[{bad}]" in msg
+
+
+def _checksum_worker(rank, world, port, n, out_q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        I0, I1 = _pairs(n)
+        a, b = multi.shard_bounds(n, rank, world)
+        local = torch.from_numpy(_fake_compute(I0[a:b], I1[a:b]))
+        full = multi.gather_flow_tensor(local, n, rank, world)
+        sums = multi.gather_checksums(multi.flow_checksum(local), rank, world)
+        if rank == 0:
+            ok = []
+            for r in range(world):
+                ra, rb = multi.shard_bounds(n, r, world)
+                ok.append(torch.equal(multi.flow_checksum(full[ra:rb]), sums[r]))
+            # a corrupted shard is detected
+            bad = full[0:multi.shard_bounds(n, 0, world)[1]].clone()
+            bad.view(-1)[5] += 1.0
+            ok.append(not torch.equal(multi.flow_checksum(bad), sums[0]))
+            out_q.put(ok)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 8), (3, 7)])
+def test_gloo_gather_checksums_verify_shards(world, n):
+    # bench.py's gather verification: per-rank bit-level checksums vs rank 0's
+    # checksums of the gathered shards
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_checksum_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok)
