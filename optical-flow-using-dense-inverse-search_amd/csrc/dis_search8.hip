@@ -212,6 +212,23 @@ __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&
     }
 }
 
+// Correctly rounded a / b for the per-patch LU pivots b, given r = RN(1 / b)
+// (one full division per patch instead of one per update): q0 = a*r is
+// within 2 ulp, one fma correction makes it faithful, and Markstein's step
+// (exact remainder e = a - b*q1, then RN(q1 + e*r)) rounds it correctly
+// (Markstein 1990; Muller et al., Handbook of FP Arithmetic, thm. 4.12),
+// given no over/underflow in the remainders -- the patch sums here are
+// image-scale. a = +-0 keeps q0 (the fma steps would turn -0 into +0);
+// b = 0 gives r = inf and NaN instead of +-inf, which the outlier test
+// resets exactly like the reference's inf.
+__device__ __forceinline__ float div_pre(float a, float b, float r)
+{
+    const float q0 = a * r;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
+    const float q2 = __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
+    return a == 0.0f ? q0 : q2;
+}
+
 // Wave-wide min/max of an int (all 64 lanes participate).
 __device__ __forceinline__ int wave_min(int v)
 {
@@ -314,6 +331,7 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
     const float sx = rx + u0, sy = ry + u1;
     float px = sx, py = sy;
     float r[8 * kNCol<LPP>];
+    const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;  // div_pre
     // rotated loop (warp at the top): one copy of the warp code, no peeled
     // first warp holding extra registers
     for (int counter = 1;; ++counter) {
@@ -326,7 +344,14 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
             b1 = b1 - bt1;
         }
         float d0, d1;
-        lu2_solve(lu, b0, b1, &d0, &d1);
+        {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
+            float c0 = lu.swap ? b1 : b0, c1 = lu.swap ? b0 : b1;
+            c1 = c1 - lu.l10 * c0;
+            c1 = div_pre(c1, lu.u11, r11);
+            c0 = c0 - c1 * lu.u01;
+            d0 = div_pre(c0, lu.u00, r00);
+            d1 = c1;
+        }
         u0 = u0 - d0;
         u1 = u1 - d1;
         px = rx + u0;
@@ -354,8 +379,14 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 
 }  // namespace
 
+#ifndef DIS_FB_WAVES
+#define DIS_FB_WAVES 3
+#endif
+#ifndef DIS_SPLIT_FB
+#define DIS_SPLIT_FB 1
+#endif
 template <int LPP, bool kFallback>
-constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? 3 : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
+constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? DIS_FB_WAVES : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
 
 // LDS of one workgroup (block of patches)
 template <int LPP>
@@ -768,7 +799,7 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     if (L != 1 && (7 * a.steps + 11) * (7 * a.steps + 10) > kTileH * kTSMax<2>) return hipErrorInvalidValue;
     const int bx = L == 1 ? kBX<1> : kBX<2>;
     dim3 grid((a.npw + bx - 1) / bx, (a.nph + kBY - 1) / kBY, batch);
-    const bool split = (L == 1 || L == 2) && a.fb_count && a.fb_list;
+    const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
     if (a.paper)
