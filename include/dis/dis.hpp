@@ -103,6 +103,8 @@ public:
         check(dis_calc_batch_u8(ctx_, n, I0, I1, stride, pair_stride, flow, where, stream));
     }
     void set_concurrency(int streams) { check(dis_set_concurrency(ctx_, streams)); }
+    // DIS_PRECISION_EXACT (default) or DIS_PRECISION_FMA (dis_abi.h)
+    void set_precision(int mode) { check(dis_set_precision(ctx_, mode)); }
 
     const dis_params& params() const { return params_; }
     int width() const { return width_; }

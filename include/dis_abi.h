@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 3
+#define DIS_ABI_VERSION 4
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -160,6 +160,18 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * where the 16x8-patch block fits, grid step <= 7; else 2). All are
  * bit-identical; the switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
+
+/* Arithmetic of the patch_size-8 search kernels (ABI v4; no reference
+ * counterpart -- the reference's own rounding is DIS_PRECISION_EXACT):
+ *   DIS_PRECISION_EXACT (default): every float operation separately rounded in
+ *     the reference's order -- bit-identical to the oracle;
+ *   DIS_PRECISION_FMA: the bilinear warp, the steepest-descent and Hessian dot
+ *     products contracted into fma, the LU solve by the pivots' reciprocals --
+ *     within the stated tolerance of the reference (mean EPE
+ *     <= 3.3e-4 px, p99.9 <= 5.1e-2 px, patch flips <= 0.014 %), faster.
+ * Generic kernels (other patch sizes) and paper mode always run exact. */
+typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;
+dis_status dis_set_precision(dis_ctx* ctx, int mode);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
 dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);
 

@@ -66,6 +66,7 @@ struct Search8Args {
     int paper;                // template-subtracted residual (k_search8<.., kPaper>)
     const float2* u_init;     // non-null (paper mode): per-patch initial u from k_paper_init, patch-id
     long long init_stride;    //   order, float2 per pair
+    int fma;                  // DIS_PRECISION_FMA: contracted warp / dot products, reciprocal solve
 };
 
 // Paper mode's coarse-to-fine initialisation of level l:

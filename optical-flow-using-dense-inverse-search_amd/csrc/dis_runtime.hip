@@ -134,6 +134,7 @@ struct dis_ctx {
     hipStream_t own = nullptr;
     static constexpr int kMaxSub = 8;
     int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
+    int precision = 0;                   // dis_set_precision: DIS_PRECISION_EXACT / _FMA
     hipStream_t sub[kMaxSub] = {};
     hipEvent_t fork = nullptr;
     // end of the previous call's work on its stream: every call first orders
@@ -461,6 +462,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             }
             b.iters = g.iters;
             b.norm = g.norm;
+            b.fma = (c->precision == DIS_PRECISION_FMA && !paper) ? 1 : 0;
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
@@ -923,6 +925,15 @@ dis_status dis_set_concurrency(dis_ctx* c, int streams)
     if (streams < 1 || streams > dis_ctx::kMaxSub)
         return fail(DIS_ERR_INVALID_ARGUMENT, "streams must be in [1, 8]");
     c->nsub = streams;
+    return DIS_OK;
+}
+
+dis_status dis_set_precision(dis_ctx* c, int mode)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (mode != DIS_PRECISION_EXACT && mode != DIS_PRECISION_FMA)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "precision must be DIS_PRECISION_EXACT or DIS_PRECISION_FMA");
+    c->precision = mode;
     return DIS_OK;
 }
 

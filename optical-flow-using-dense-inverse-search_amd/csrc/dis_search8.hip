@@ -174,30 +174,32 @@ __device__ __forceinline__ float patch_sum(const float (&x)[8 * kNCol<LPP>])
 
 // Eigen order of sum(g .* r): each product rounded, then accumulated in the
 // patch_sum order; products are formed inside the chains (no 32-value temp).
-template <int LPP, typename Fn>
+// kFma (DIS_PRECISION_FMA): a + g*r contracted into one fma per product.
+template <int LPP, bool kFma = false, typename Fn>
 __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&& r)
 {
+    auto mac = [](float acc, float x, float y) { return kFma ? __builtin_fmaf(x, y, acc) : acc + x * y; };
     if constexpr (LPP == 1) {
         float A[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             A[c] = g[8 * c] * r(8 * c);
 #pragma unroll
-            for (int j = 1; j < 8; ++j) A[c] = A[c] + g[8 * c + j] * r(8 * c + j);
+            for (int j = 1; j < 8; ++j) A[c] = mac(A[c], g[8 * c + j], r(8 * c + j));
         }
         return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
     } else if constexpr (LPP == 8) {
         float a = g[0] * r(0);
 #pragma unroll
-        for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
+        for (int j = 1; j < 8; ++j) a = mac(a, g[j], r(j));
         return reduce_cols<8>(a);
     } else if constexpr (LPP == 4) {
         float a = g[0] * r(0);
 #pragma unroll
-        for (int j = 1; j < 8; ++j) a = a + g[j] * r(j);
+        for (int j = 1; j < 8; ++j) a = mac(a, g[j], r(j));
         float b = g[8] * r(8);
 #pragma unroll
-        for (int j = 9; j < 16; ++j) b = b + g[j] * r(j);
+        for (int j = 9; j < 16; ++j) b = mac(b, g[j], r(j));
         return reduce_cols<4>(a + b);
     } else {
         float C[4];
@@ -205,7 +207,7 @@ __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&
         for (int ci = 0; ci < 4; ++ci) {
             float a = g[8 * ci] * r(8 * ci);
 #pragma unroll
-            for (int j = 1; j < 8; ++j) a = a + g[8 * ci + j] * r(8 * ci + j);
+            for (int j = 1; j < 8; ++j) a = mac(a, g[8 * ci + j], r(8 * ci + j));
             C[ci] = a + quad_perm<kQuadXor1>(a);
         }
         return (C[0] + C[2]) + (C[1] + C[3]);
@@ -267,9 +269,10 @@ __device__ __forceinline__ Warp warp_coefs(float x, float y)
 
 // `tap(k, c)` returns the target image at row Y-5+k (k = 0..8) and column
 // X-5 + qb + c, qb = the lane's first pixel column (LPP 1: 0, LPP 2: 4q, else q).
-template <int LPP, bool kFence = false, typename Tap>
+template <int LPP, bool kFence = false, bool kFma = false, typename Tap>
 __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[8 * kNCol<LPP>])
 {
+    auto mac = [](float acc, float x, float y) { return kFma ? __builtin_fmaf(x, y, acc) : acc + x * y; };
     if constexpr (LPP == 4 || LPP == 8) {
 #pragma unroll
         for (int s = 0; s < kNCol<LPP>; ++s) {
@@ -283,9 +286,9 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
             for (int j = 0; j < 8; ++j) {
                 // row Y-4+j: A = va[j+1], B = vb[j+1]; row Y-5+j: C = va[j], D = vb[j]
                 float t = w.w3 * va[j + 1];
-                t = t + w.w2 * vb[j + 1];
-                t = t + w.w1 * va[j];
-                t = t + w.w0 * vb[j];
+                t = mac(t, w.w2, vb[j + 1]);
+                t = mac(t, w.w1, va[j]);
+                t = mac(t, w.w0, vb[j]);
                 r[8 * s + j] = t;
             }
         }
@@ -302,9 +305,9 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
 #pragma unroll
             for (int ci = 0; ci < NC; ++ci) {
                 float t = w.w3 * cur[ci + 1];
-                t = t + w.w2 * cur[ci];
-                t = t + w.w1 * prev[ci + 1];
-                t = t + w.w0 * prev[ci];
+                t = mac(t, w.w2, cur[ci]);
+                t = mac(t, w.w1, prev[ci + 1]);
+                t = mac(t, w.w0, prev[ci]);
                 r[8 * ci + j] = t;
             }
 #pragma unroll
@@ -322,7 +325,7 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
 // The per-patch iteration (src/patch.cpp:156-203) with a given tap source.
 // kPaper: b -= (bt0, bt1), the template part of the
 // template-subtracted residual (see search_block).
-template <int LPP, bool kFence, bool kPaper, typename TapAt>
+template <int LPP, bool kFence, bool kPaper, bool kFma, typename TapAt>
 __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, const float (&gx)[8 * kNCol<LPP>],
                                         const float (&gy)[8 * kNCol<LPP>], float rx, float ry, float ix, float iy,
                                         float bt0, float bt1, float* pu0, float* pu1, TapAt&& tap_at)
@@ -336,9 +339,9 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
     // first warp holding extra registers
     for (int counter = 1;; ++counter) {
         const Warp w = warp_coefs(px, py);
-        warp_patch<LPP, kFence>(w, a.norm, tap_at(w), r);
-        float b0 = patch_dot<LPP>(gx, [&](int j) { return r[j]; });
-        float b1 = patch_dot<LPP>(gy, [&](int j) { return r[j]; });
+        warp_patch<LPP, kFence, kFma>(w, a.norm, tap_at(w), r);
+        float b0 = patch_dot<LPP, kFma>(gx, [&](int j) { return r[j]; });
+        float b1 = patch_dot<LPP, kFma>(gy, [&](int j) { return r[j]; });
         if constexpr (kPaper) {
             b0 = b0 - bt0;
             b1 = b1 - bt1;
@@ -347,9 +350,15 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
         {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
             float c0 = lu.swap ? b1 : b0, c1 = lu.swap ? b0 : b1;
             c1 = c1 - lu.l10 * c0;
-            c1 = div_pre(c1, lu.u11, r11);
-            c0 = c0 - c1 * lu.u01;
-            d0 = div_pre(c0, lu.u00, r00);
+            if constexpr (kFma) {  // tolerance mode: multiply by the rounded reciprocal
+                c1 = c1 * r11;
+                c0 = __builtin_fmaf(-c1, lu.u01, c0);
+                d0 = c0 * r00;
+            } else {
+                c1 = div_pre(c1, lu.u11, r11);
+                c0 = c0 - c1 * lu.u01;
+                d0 = div_pre(c0, lu.u00, r00);
+            }
             d1 = c1;
         }
         u0 = u0 - d0;
@@ -403,7 +412,7 @@ struct BlockLds {
 // is appended to the launch's fallback list (a.fb_count / a.fb_list) for
 // k_search8_fb and nothing is written here (keeps this kernel's registers
 // low enough for 4 waves per SIMD at LPP 2).
-template <int LPP, bool kFallback, bool kPaper>
+template <int LPP, bool kFallback, bool kPaper, bool kFma = false>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -608,9 +617,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     }
     LU2 lu;
     {
-        const float h00 = patch_dot<LPP>(gdx, [&](int j) { return gdx[j]; });
-        const float h01 = patch_dot<LPP>(gdx, [&](int j) { return gdy[j]; });
-        const float h11 = patch_dot<LPP>(gdy, [&](int j) { return gdy[j]; });
+        const float h00 = patch_dot<LPP, kFma>(gdx, [&](int j) { return gdx[j]; });
+        const float h01 = patch_dot<LPP, kFma>(gdx, [&](int j) { return gdy[j]; });
+        const float h11 = patch_dot<LPP, kFma>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
     const float sx = rx + ix, sy = ry + iy;
@@ -666,7 +675,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         __syncthreads();
         if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
-            iterate<LPP, false, kPaper>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
+            iterate<LPP, false, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
 #ifdef DIS_EXP_TAPBANKS  // experiment: lane-fixed, conflict-free tap addresses (wrong values)
                 const float* base = tile + (lane & 31) + ((w.X & 1) << 5) + 0 * qb;
 #else
@@ -678,7 +687,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     } else if constexpr (kFallback) {
         if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
-            iterate<LPP, true, kPaper>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
+            iterate<LPP, true, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
                 const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
                 return [=](int k, int c) {
                     return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
@@ -697,12 +706,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 }
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
-template <int LPP, bool kFallback, bool kPaper = false>
+template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
-    search_block<LPP, kFallback, kPaper>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+    search_block<LPP, kFallback, kPaper, kFma>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
@@ -710,7 +719,7 @@ k_search8(Search8Args a)
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
 // its workgroups cannot take the slots another stream's search kernel frees,
 // and the (usually empty) launch waited 70-150 us for that kernel to drain.
-template <int LPP, bool kPaper = false>
+template <int LPP, bool kPaper = false, bool kFma = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
 __attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
@@ -721,7 +730,7 @@ k_search8_fb(Search8Args a)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int e = a.fb_list[i];
         const int bx = e % nbx, t = e / nbx;
-        search_block<LPP, true, kPaper>(a, bx, t % nby, t / nby, S);
+        search_block<LPP, true, kPaper, kFma>(a, bx, t % nby, t / nby, S);
         __syncthreads();  // LDS reuse by the next listed block
     }
 }
@@ -764,28 +773,28 @@ bool search8_lpp1_fits(int steps)
     return (15 * steps + 11) * (7 * steps + 10) <= kTileH * kTSMax<1>;
 }
 
-template <bool kPaper>
+template <bool kPaper, bool kFma>
 static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid, dim3 fb_grid, hipStream_t s,
                              Timing t)
 {
     if (L == 1) {
         if (split) {
-            DIS_LAUNCH(t, (k_search8<1, false, kPaper>), grid, dim3(kThreads<1>), 0, s, a);
-            hipLaunchKernelGGL((k_search8_fb<1, kPaper>), fb_grid, dim3(kThreads<1>), 0, s, a);
+            DIS_LAUNCH(t, (k_search8<1, false, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
         } else {
-            DIS_LAUNCH(t, (k_search8<1, true, kPaper>), grid, dim3(kThreads<1>), 0, s, a);
+            DIS_LAUNCH(t, (k_search8<1, true, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
         }
     } else if (L == 2) {
         if (split) {
-            DIS_LAUNCH(t, (k_search8<2, false, kPaper>), grid, dim3(kThreads<2>), 0, s, a);
-            hipLaunchKernelGGL((k_search8_fb<2, kPaper>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
-            DIS_LAUNCH(t, (k_search8<2, true, kPaper>), grid, dim3(kThreads<2>), 0, s, a);
+            DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
         }
     } else if (L == 4) {
-        DIS_LAUNCH(t, (k_search8<4, true, kPaper>), grid, dim3(kThreads<4>), 0, s, a);
+        DIS_LAUNCH(t, (k_search8<4, true, kPaper, kFma>), grid, dim3(kThreads<4>), 0, s, a);
     } else {
-        DIS_LAUNCH(t, (k_search8<8, true, kPaper>), grid, dim3(kThreads<8>), 0, s, a);
+        DIS_LAUNCH(t, (k_search8<8, true, kPaper, kFma>), grid, dim3(kThreads<8>), 0, s, a);
     }
 }
 
@@ -802,10 +811,12 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
-    if (a.paper)
-        launch_search8_t<true>(a, L, split, grid, fb_grid, s, t);
+    if (a.paper)  // paper mode has no tolerance variant: always the exact kernels
+        launch_search8_t<true, false>(a, L, split, grid, fb_grid, s, t);
+    else if (a.fma)
+        launch_search8_t<false, true>(a, L, split, grid, fb_grid, s, t);
     else
-        launch_search8_t<false>(a, L, split, grid, fb_grid, s, t);
+        launch_search8_t<false, false>(a, L, split, grid, fb_grid, s, t);
     return hipGetLastError();
 }
 

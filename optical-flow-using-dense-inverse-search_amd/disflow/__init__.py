@@ -46,6 +46,8 @@ MEM_DEVICE = 1
 
 STAGE_IMG0, STAGE_IMG1, STAGE_DX0, STAGE_DY0, STAGE_PATCH_U, STAGE_DENSE = range(6)
 
+PRECISION_EXACT, PRECISION_FMA = 0, 1
+
 KERNEL_PYRAMID, KERNEL_SEARCH, KERNEL_SEARCH_FINEST, KERNEL_DENSIFY = range(4)
 
 # Every symbol include/dis_abi.h declares (checked by tests/test_abi.py).
@@ -54,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "dis_workload_info", "dis_create", "dis_destroy", "dis_calc_u8", "dis_calc_batch_u8",
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
-    "dis_set_concurrency", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
+    "dis_set_concurrency", "dis_set_precision", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
 )
 
 
@@ -147,6 +149,8 @@ def lib() -> ctypes.CDLL:
         L.dis_set_debug.argtypes = [V, I]
         L.dis_set_kernel_variant.argtypes = [V, I]
         L.dis_set_concurrency.argtypes = [V, I]
+        if L.dis_abi_version() >= 4:  # (older builds load for A/B timing only)
+            L.dis_set_precision.argtypes = [V, I]
         L.dis_stage_size.argtypes = [V, I, I, P(Z)]
         L.dis_debug_dump.argtypes = [V, I, I, I, V, Z]
         L.dis_set_kernel_timing.argtypes = [V, I]
@@ -157,7 +161,7 @@ def lib() -> ctypes.CDLL:
         L.dis_read_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
         L.dis_write_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
         for name in EXPORTED_SYMBOLS:
-            if name not in ("dis_abi_version", "dis_last_error"):
+            if name not in ("dis_abi_version", "dis_last_error") and hasattr(L, name):
                 getattr(L, name).restype = I
         _lib = L
     return _lib
@@ -280,6 +284,11 @@ class DenseInverseSearch:
     def set_concurrency(self, streams: int) -> None:
         """Sub-batch streams per calc (1..8); results are identical for any value."""
         _check(lib().dis_set_concurrency(self._ctx, streams))
+
+    def set_precision(self, mode: int) -> None:
+        """PRECISION_EXACT (default, bit-identical to the reference order) or
+        PRECISION_FMA (contracted search arithmetic, within the stated tolerance)."""
+        _check(lib().dis_set_precision(self._ctx, mode))
 
     def set_debug(self, on: bool = True) -> None:
         _check(lib().dis_set_debug(self._ctx, int(on)))

@@ -8,6 +8,8 @@ resident in HBM, batch per call as given, `steps` timed calls after warmup.
   config 3  3840x2160  MEDIUM
   config 5  3840x2160  SLOW + variational refinement (3 fixed-point iterations per level)
   2p        1920x1080  MEDIUM in paper mode
+  2f / 3f   configs 2 / 3 with DIS_PRECISION_FMA (contracted search arithmetic,
+            within the stated tolerance; tests/test_gpu_tolerance.py)
   colour    1920x1080  Middlebury colour coding of 32 flow fields (dis_flow_color)
 """
 import argparse
@@ -29,10 +31,14 @@ CONFIGS = {
     "3": ("3840x2160 MEDIUM", 3840, 2160, "MEDIUM", 8),
     "5": ("3840x2160 SLOW + variational refinement", 3840, 2160, "SLOW", 2),
     "2p": ("1920x1080 MEDIUM paper mode", 1920, 1080, "MEDIUM", 32, 1),
+    "2f": ("1920x1080 MEDIUM, DIS_PRECISION_FMA", 1920, 1080, "MEDIUM", 32, 0, 1),
+    "3f": ("3840x2160 MEDIUM, DIS_PRECISION_FMA", 3840, 2160, "MEDIUM", 8, 0, 1),
 }
+FMA_PEAK = 157.3  # TFLOP/s, vector f32 with FMA counted as 2 (MI355X_MICROARCH.md)
+EXACT_PEAK = 78.6  # non-FMA f32 issue peak (one op per lane per instruction)
 
 
-def run(name, W, H, preset, B, steps, warmup, paper=0):
+def run(name, W, H, preset, B, steps, warmup, paper=0, fma=0):
     dev = torch.device("cuda", 0)
     p = disflow.preset_params(disflow.Preset[preset], W, H)
     p.paper_mode = paper
@@ -41,6 +47,8 @@ def run(name, W, H, preset, B, steps, warmup, paper=0):
     d1 = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
     out = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
     eng = disflow.DenseInverseSearch(p, W, H, max_batch=B)
+    if fma:
+        eng.set_precision(disflow.PRECISION_FMA)
     s = torch.cuda.current_stream(dev)
     for _ in range(warmup):
         eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
@@ -51,8 +59,25 @@ def run(name, W, H, preset, B, steps, warmup, paper=0):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     wl = disflow.workload(p, W, H)
+    # finest-level search launch, one stream, HIP dispatch events (as bench.py)
+    eng.set_concurrency(1)
+    eng.set_kernel_timing(True)
+    for _ in range(3):
+        eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
+    eng.set_kernel_timing(False)
+    launch_ms = ms_f / max(n_f, 1)
+    flops = wl["search_flops_finest"] * B
+    achieved = flops / (launch_ms * 1e-3) / 1e12
+    peak = FMA_PEAK if fma else EXACT_PEAK
     eng.close()
-    return {"config": name, "preset": preset, "knobs": {"C": p.coarsest_scale, "F": p.finest_scale,
+    return {"config": name, "preset": preset, "precision": "fma" if fma else "exact",
+            "finest_search": {"avg_launch_ms": launch_ms, "algorithmic_tflops": achieved, "peak": peak,
+                              "frac": achieved / peak,
+                              "note": "algorithmic ops of the reference (each add/mul 1) / launch time; peak "
+                                      + ("157.3 (FMA = 2 ops)" if fma else "78.6 (non-FMA issue)")},
+            "knobs": {"C": p.coarsest_scale, "F": p.finest_scale,
                                                         "it": p.iterations, "overlap": p.patch_overlap,
                                                         "var_refine_iters": p.var_refine_iters,
                                                         "paper_mode": p.paper_mode},
@@ -88,7 +113,7 @@ def run_colour(steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,2,3,5,2p,colour")
+    ap.add_argument("--configs", default="1,2,3,5,2p,2f,3f,colour")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
