@@ -105,6 +105,7 @@ public:
     void set_concurrency(int streams) { check(dis_set_concurrency(ctx_, streams)); }
     // DIS_PRECISION_EXACT (default) or DIS_PRECISION_FMA (dis_abi.h)
     void set_precision(int mode) { check(dis_set_precision(ctx_, mode)); }
+    void set_graphs(bool on) { check(dis_set_graphs(ctx_, on ? 1 : 0)); }
 
     const dis_params& params() const { return params_; }
     int width() const { return width_; }

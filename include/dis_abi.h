@@ -170,6 +170,15 @@ dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
  *     within the stated tolerance of the reference (mean EPE
  *     <= 3.3e-4 px, p99.9 <= 5.1e-2 px, patch flips <= 0.014 %), faster.
  * Generic kernels (other patch sizes) and paper mode always run exact. */
+/* HIP graphs (ABI v4): with graphs on (the default) a batch call is captured
+ * once per (n, frame/flow pointers and strides, concurrency, precision,
+ * variant) and replayed as one graph -- the fork into the sub-batch streams,
+ * every level's launches and the join -- instead of ~25 eager launches; a
+ * changed key re-captures (the executable graph is updated in place). Kernel
+ * timing, debug dumps and variational refinement run eagerly. Results do not
+ * depend on this setting. */
+dis_status dis_set_graphs(dis_ctx* ctx, int enable);
+
 typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;
 dis_status dis_set_precision(dis_ctx* ctx, int mode);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);

@@ -152,6 +152,18 @@ struct dis_ctx {
         int n = -1, p0 = -1;
     } vrg[kMaxSub][dis::kMaxLevels];
     hipStream_t cap = nullptr;  // capture-only stream
+    // The whole batch call (both sub-batches' pyramid, level searches and
+    // output, with the fork/join) replayed as one HIP graph, captured on the
+    // first call with a given key and re-captured (exec updated in place) when
+    // the key changes: dis_set_graphs, default on.
+    int graphs = 1;
+    struct MainGraph {
+        hipGraphExec_t exec = nullptr;
+        int n = -1, nsub = -1, precision = -1, variant = -1;
+        const void *i0 = nullptr, *i1 = nullptr;
+        void* flow = nullptr;
+        size_t stride = 0, pair_stride = 0;
+    } mg;
     // workspace (device)
     float* img0 = nullptr;
     float* img1 = nullptr;
@@ -586,7 +598,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
 // (VALU-bound) instead of contending with the other pyramids for HBM, and
 // k-1's output kernel runs beside k's search.
 dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
-                       size_t pair_stride, float2* flow, hipStream_t s)
+                       size_t pair_stride, float2* flow, hipStream_t s, bool capturing = false)
 {
     // refinement: one stream. Its many short bandwidth-bound kernels stall
     // behind a co-running sub-batch's long search launches (measured on
@@ -595,13 +607,14 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     std::vector<int> stages = {kStageFront};
     for (int l = c->g.C; l >= c->g.F; --l) stages.push_back(l);
     stages.push_back(kStageBack);
-    if (c->done_pending) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
+    if (c->done_pending && !capturing) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     if (S <= 1) {
         for (int st : stages) {
             dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
             if (r != DIS_OK) return r;
         }
         c->last_batch = n;
+        if (capturing) return DIS_OK;
         DIS_HIP(hipEventRecord(c->done, s));
         c->done_pending = true;
         return DIS_OK;
@@ -633,6 +646,65 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
         DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     }
+    c->last_batch = n;
+    if (capturing) return DIS_OK;
+    DIS_HIP(hipEventRecord(c->done, s));
+    c->done_pending = true;
+    return DIS_OK;
+}
+
+// run_batches as a replayed HIP graph (see dis_ctx::MainGraph). Eager when
+// graphs are off, under kernel timing (per-dispatch events), debug dumps or
+// variational refinement (its own per-level graphs).
+dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
+                             size_t pair_stride, float2* flow, hipStream_t s)
+{
+    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap)
+        return run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
+    auto& G = c->mg;
+    const bool hit = G.exec && G.n == n && G.i0 == I0 && G.i1 == I1 && G.flow == flow && G.stride == stride &&
+                     G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
+                     G.variant == c->variant;
+    if (!hit) {
+        hipGraph_t graph = nullptr;
+        DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+        const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true);
+        const hipError_t e = hipStreamEndCapture(c->cap, &graph);
+        if (r != DIS_OK) {
+            if (graph) hipGraphDestroy(graph);
+            return r;
+        }
+        DIS_HIP(e);
+        hipError_t e2 = hipErrorUnknown;
+        if (G.exec) {  // same topology (same n and sub-batches): update the parameters in place
+            hipGraphExecUpdateResult res;
+            hipGraphNode_t bad = nullptr;
+            e2 = hipGraphExecUpdate(G.exec, graph, &bad, &res);
+            if (e2 != hipSuccess) {
+                (void)hipGetLastError();
+                hipGraphExecDestroy(G.exec);
+                G.exec = nullptr;
+            }
+        }
+        if (!G.exec) e2 = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e2 != hipSuccess) {
+            G.exec = nullptr;
+            G.n = -1;
+            DIS_HIP(e2);
+        }
+        G.n = n;
+        G.i0 = I0;
+        G.i1 = I1;
+        G.flow = flow;
+        G.stride = stride;
+        G.pair_stride = pair_stride;
+        G.nsub = c->nsub;
+        G.precision = c->precision;
+        G.variant = c->variant;
+    }
+    if (c->done_pending) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
+    DIS_HIP(hipGraphLaunch(G.exec, s));
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
@@ -830,8 +902,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
     // robin at creation, and an extra stream created before sub[] shifted
     // sub[1] onto the caller's (null stream's) queue, serialising the two
     // sub-batches (measured: 20.1k -> 15.5k pairs/s at 1080p MEDIUM).
-    if (ok && params->var_refine_iters > 0)
-        ok = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking) == hipSuccess;
+    if (ok) ok = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         free_ws(c);
         for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
@@ -868,6 +939,7 @@ dis_status dis_destroy(dis_ctx* c)
     for (auto& row : c->vrg)
         for (auto& G : row)
             if (G.exec) hipGraphExecDestroy(G.exec);
+    if (c->mg.exec) hipGraphExecDestroy(c->mg.exec);
     if (c->cap) hipStreamDestroy(c->cap);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
@@ -887,8 +959,8 @@ dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     if (n > 1 && pair_stride < stride * H) return fail(DIS_ERR_INVALID_ARGUMENT, "pair_stride too small");
     DIS_HIP(hipSetDevice(c->device));
     if (where == DIS_MEM_DEVICE) {
-        return run_batches(c, n, I0, I1, stride, pair_stride, reinterpret_cast<float2*>(flow),
-                         reinterpret_cast<hipStream_t>(stream));
+        return run_batches_graph(c, n, I0, I1, stride, pair_stride, reinterpret_cast<float2*>(flow),
+                                 reinterpret_cast<hipStream_t>(stream));
     }
     if (where != DIS_MEM_HOST) return fail(DIS_ERR_INVALID_ARGUMENT, "bad dis_mem");
     hipStream_t s = c->own;
@@ -899,7 +971,7 @@ dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         DIS_HIP(hipMemcpy2DAsync(c->in1 + k * fsz, W, I1 + k * pair_stride, stride, W, H,
                                  hipMemcpyHostToDevice, s));
     }
-    dis_status st = run_batches(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
+    dis_status st = run_batches_graph(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
     if (st != DIS_OK) return st;
     DIS_HIP(hipMemcpyAsync(flow, c->out, sizeof(float2) * fsz * n, hipMemcpyDeviceToHost, s));
     DIS_HIP(hipStreamSynchronize(s));
@@ -925,6 +997,13 @@ dis_status dis_set_concurrency(dis_ctx* c, int streams)
     if (streams < 1 || streams > dis_ctx::kMaxSub)
         return fail(DIS_ERR_INVALID_ARGUMENT, "streams must be in [1, 8]");
     c->nsub = streams;
+    return DIS_OK;
+}
+
+dis_status dis_set_graphs(dis_ctx* c, int enable)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    c->graphs = enable ? 1 : 0;
     return DIS_OK;
 }
 

@@ -164,6 +164,46 @@ def test_calls_on_different_streams_do_not_race(disflow_mod):
         assert np.array_equal(gy.view(np.uint32), ey.view(np.uint32))
 
 
+def test_graph_replay_matches_eager_and_tracks_its_key(disflow_mod):
+    # dis_set_graphs (default on): a batch call is captured once per key and
+    # replayed; new buffers, batch sizes, concurrency and precision re-capture.
+    # Every replay must equal the eager path bit for bit.
+    import torch
+    W, H, B = 640, 480, 4
+    d = disflow_mod
+    p = d.preset_params(d.Preset.MEDIUM, W, H)
+    pairs = [d.synth_pair(70 + k, W, H) for k in range(B)]
+    X0 = np.stack([a for a, _ in pairs])
+    X1 = np.stack([b for _, b in pairs])
+    eager = d.DenseInverseSearch(p, W, H, max_batch=B)
+    eager.set_graphs(False)
+    ref = eager.calc_batch(X0, X1)
+    eng = d.DenseInverseSearch(p, W, H, max_batch=B)
+    s = torch.cuda.current_stream()
+    bufs = [(torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda(),
+             torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")) for _ in range(2)]
+    for rep in range(3):
+        for k, (d0, d1, out) in enumerate(bufs):  # alternating keys: re-capture every call
+            for n in (B, 2):
+                out.fill_(float("nan"))
+                eng.calc_device(n, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+                torch.cuda.synchronize()
+                assert np.array_equal(out[:n].cpu().numpy().view(np.uint32), ref[:n].view(np.uint32)), (rep, k, n)
+    d0, d1, out = bufs[0]
+    for streams in (1, 3):
+        eng.set_concurrency(streams)
+        for _ in range(2):  # capture, then replay
+            out.fill_(float("nan"))
+            eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), streams
+    eng.set_precision(d.PRECISION_FMA)  # a new key: the FMA kernels must run, not the cached exact graph
+    eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert not np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(eng.calc_batch(X0, X1).view(np.uint32), out.cpu().numpy().view(np.uint32))
+
+
 def test_medium_1080p_full_size_bitexact(disflow_mod, oracle):
     # BASELINE config 2 workload at full size against the oracle (a few seconds on CPU)
     W, H = 1920, 1080

@@ -59,6 +59,10 @@ def main():
                 eng.set_concurrency(int(val))
             elif k == "variant":
                 eng.set_variant(int(val))
+            elif k == "graphs":
+                eng.set_graphs(bool(int(val)))
+            elif k == "fma":
+                eng.set_precision(int(val))
             else:
                 raise SystemExit(f"unknown option {k}")
         engines.append((v, L, eng))
