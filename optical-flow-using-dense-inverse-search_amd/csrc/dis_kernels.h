@@ -67,6 +67,13 @@ struct Search8Args {
     const float2* u_init;     // non-null (paper mode): per-patch initial u from k_paper_init, patch-id
     long long init_stride;    //   order, float2 per pair
     int fma;                  // DIS_PRECISION_FMA: contracted warp / dot products, reciprocal solve
+    // compat path (dis_flow_from_pyramids): non-null = the caller's physically
+    // padded planes (pad pixels on every side, row stride W + 2 pad; plane_off
+    // = the padded plane's start): template gradients from gdx/gdy_plane, I1
+    // taps from the padded img1 plane
+    const float* gdx_plane;
+    const float* gdy_plane;
+    int pad;
 };
 
 // Paper mode's coarse-to-fine initialisation of level l:

@@ -746,6 +746,77 @@ bool sub_streams(int device, hipStream_t (&out)[dis_ctx::kMaxSub])
     return true;
 }
 
+// Compat path workspace: one per device for the process, grown on demand.
+struct CompatWs {
+    float *dx = nullptr, *dy = nullptr, *i1 = nullptr;
+    float2 *pu = nullptr, *dense = nullptr;
+    int* fb = nullptr;
+    size_t planes = 0, u = 0, d = 0, nfb = 0;
+    hipStream_t stream = nullptr;
+    bool reserve(size_t p, size_t nu, size_t nd, size_t nf)
+    {
+        if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+        if (p > planes) {
+            hipFree(dx);
+            hipFree(dy);
+            hipFree(i1);
+            dx = dy = i1 = nullptr;
+            planes = 0;
+            if (hipMalloc(&dx, sizeof(float) * p) != hipSuccess || hipMalloc(&dy, sizeof(float) * p) != hipSuccess ||
+                hipMalloc(&i1, sizeof(float) * p) != hipSuccess)
+                return false;
+            planes = p;
+        }
+        if (nu > u) {
+            hipFree(pu);
+            pu = nullptr;
+            u = 0;
+            if (hipMalloc(&pu, sizeof(float2) * nu) != hipSuccess) return false;
+            u = nu;
+        }
+        if (nd > d) {
+            hipFree(dense);
+            dense = nullptr;
+            d = 0;
+            if (hipMalloc(&dense, sizeof(float2) * nd) != hipSuccess) return false;
+            d = nd;
+        }
+        if (nf > nfb) {
+            hipFree(fb);
+            fb = nullptr;
+            nfb = 0;
+            if (hipMalloc(&fb, sizeof(int) * nf) != hipSuccess) return false;
+            nfb = nf;
+        }
+        return true;
+    }
+};
+std::mutex compat_mu;
+CompatWs& compat_ws(int device)
+{
+    static std::map<int, CompatWs> ws;  // process lifetime (freed by the driver at exit)
+    return ws[device];
+}
+
+dis::DensifyArgs densify_level(const dis::Geometry& g, int l, float2* pu, float2* dense)
+{
+    const dis::LevelGeom& L = g.lv[l];
+    dis::DensifyArgs d{};
+    d.u = pu + L.u_off;
+    d.dense = dense + L.dense_off;
+    d.u_stride = g.u_stride;
+    d.dense_stride = g.dense_stride;
+    d.W = L.W;
+    d.H = L.H;
+    d.ps = g.ps;
+    d.steps = L.steps;
+    d.npw = L.npw;
+    d.nph = L.nph;
+    d.offw = L.offw;
+    d.offh = L.offh;
+    return d;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1152,42 +1223,74 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(DIS_ERR_DEVICE, "no HIP device");
     if (device < 0 || device >= ndev) return fail(DIS_ERR_INVALID_ARGUMENT, "device index out of range");
     DIS_HIP(hipSetDevice(device));
-    float *dx = nullptr, *dy = nullptr, *i1 = nullptr;
-    float2 *pu = nullptr, *dense = nullptr;
-    auto cleanup = [&]() {
-        hipFree(dx);
-        hipFree(dy);
-        hipFree(i1);
-        hipFree(pu);
-        hipFree(dense);
-    };
-    if (hipMalloc(&dx, sizeof(float) * tot) != hipSuccess || hipMalloc(&dy, sizeof(float) * tot) != hipSuccess ||
-        hipMalloc(&i1, sizeof(float) * tot) != hipSuccess ||
-        hipMalloc(&pu, sizeof(float2) * g.u_stride) != hipSuccess ||
-        hipMalloc(&dense, sizeof(float2) * g.dense_stride) != hipSuccess) {
-        cleanup();
-        return fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
-    }
-    hipStream_t s = nullptr;
-    dis_status rc = DIS_OK;
+    // per-device workspace, grown on demand and kept for the next call (the
+    // reference constructs one OpticalFlowClass per frame pair: a malloc/free
+    // per call would dominate)
+    size_t fb_n = dis::kMaxLevels;
+    for (int l = g.F; l <= g.C; ++l) fb_n += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8);
+    std::lock_guard<std::mutex> lock(compat_mu);
+    CompatWs& w = compat_ws(device);
+    if (!w.reserve(tot, g.u_stride, g.dense_stride, fb_n)) return fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
+    hipStream_t s = w.stream;
+    const bool fast = g.ps == 8;
     auto H2D = [&](float* dst, const float* src, size_t cnt) {
         return hipMemcpyAsync(dst, src, sizeof(float) * cnt, hipMemcpyHostToDevice, s);
     };
-    for (int l = finest; l <= coarsest && rc == DIS_OK; ++l) {
+    for (int l = finest; l <= coarsest; ++l) {
         const size_t cnt = (size_t)(g.lv[l].W + 2 * img_padding) * (g.lv[l].H + 2 * img_padding);
-        if (H2D(dx + poff[l], img_first_dx[l], cnt) != hipSuccess ||
-            H2D(dy + poff[l], img_first_dy[l], cnt) != hipSuccess ||
-            H2D(i1 + poff[l], img_second[l], cnt) != hipSuccess)
-            rc = fail(DIS_ERR_DEVICE, "pyramid upload failed");
+        if (H2D(w.dx + poff[l], img_first_dx[l], cnt) != hipSuccess ||
+            H2D(w.dy + poff[l], img_first_dy[l], cnt) != hipSuccess ||
+            H2D(w.i1 + poff[l], img_second[l], cnt) != hipSuccess)
+            return fail(DIS_ERR_DEVICE, "pyramid upload failed");
     }
-    for (int l = g.C; l >= g.F && rc == DIS_OK; --l) {
+    if (fast) DIS_HIP(hipMemsetAsync(w.fb, 0, sizeof(int) * dis::kMaxLevels, s));
+    size_t fb_off = dis::kMaxLevels;
+    for (int l = g.C; l >= g.F; --l) {
         const dis::LevelGeom& L = g.lv[l];
+        if (fast) {  // the patch_size-8 search on the caller's planes (Search8Args.gdx_plane)
+            dis::Search8Args b{};
+            b.img1 = w.i1;
+            b.gdx_plane = w.dx;
+            b.gdy_plane = w.dy;
+            b.pad = img_padding;
+            b.u_coarse = (l < g.C) ? w.pu + g.lv[l + 1].u_off : nullptr;
+            b.u_out = w.pu + L.u_off;
+            b.plane_stride = tot;
+            b.plane_off = poff[l];
+            b.u_stride = g.u_stride;
+            b.W = L.W;
+            b.H = L.H;
+            b.steps = L.steps;
+            b.npw = L.npw;
+            b.nph = L.nph;
+            b.offw = L.offw;
+            b.offh = L.offh;
+            if (l < g.C) {
+                b.c_npw = g.lv[l + 1].npw;
+                b.c_nph = g.lv[l + 1].nph;
+                b.c_offw = g.lv[l + 1].offw;
+                b.c_offh = g.lv[l + 1].offh;
+            }
+            b.tmp_lb = L.tmp_lb;
+            b.tmp_ub_w = L.tmp_ub_w;
+            b.tmp_ub_h = L.tmp_ub_h;
+            b.thr_sq = sqrt_threshold((float)g.ps / 2);
+            b.lanes_per_patch = search8_lanes(0, (long long)L.npw * L.nph, L.steps) == 8 ? 8 : 2;
+            b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
+            b.fb_count = w.fb + l;
+            b.fb_list = w.fb + fb_off;
+            fb_off += (size_t)((L.npw + 7) / 8) * ((L.nph + 7) / 8);
+            b.iters = g.iters;
+            b.norm = g.norm;
+            if (dis::launch_search8(b, 1, s) != hipSuccess) return fail(DIS_ERR_DEVICE, "search launch failed");
+            continue;
+        }
         dis::SearchArgs a{};
-        a.img1 = i1;
-        a.dx = dx;
-        a.dy = dy;
-        a.dense_coarse = (l < g.C) ? dense + g.lv[l + 1].dense_off : nullptr;
-        a.u_out = pu + L.u_off;
+        a.img1 = w.i1;
+        a.dx = w.dx;
+        a.dy = w.dy;
+        a.dense_coarse = (l < g.C) ? w.dense + g.lv[l + 1].dense_off : nullptr;
+        a.u_out = w.pu + L.u_off;
         a.plane_stride = tot;
         a.plane_off = poff[l];
         a.dense_stride = g.dense_stride;
@@ -1207,35 +1310,19 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
         a.outlier = (float)g.ps / 2;
         a.iters = g.iters;
         a.norm = g.norm;
-        if (dis::launch_search_generic(a, g.ps, 1, s) != hipSuccess) {
-            rc = fail(DIS_ERR_DEVICE, "search launch failed");
-            break;
-        }
-        dis::DensifyArgs d{};
-        d.u = pu + L.u_off;
-        d.dense = dense + L.dense_off;
-        d.u_stride = g.u_stride;
-        d.dense_stride = g.dense_stride;
-        d.W = L.W;
-        d.H = L.H;
-        d.ps = g.ps;
-        d.steps = L.steps;
-        d.npw = L.npw;
-        d.nph = L.nph;
-        d.offw = L.offw;
-        d.offh = L.offh;
-        if (dis::launch_densify(d, 1, s) != hipSuccess) rc = fail(DIS_ERR_DEVICE, "densify launch failed");
+        if (dis::launch_search_generic(a, g.ps, 1, s) != hipSuccess) return fail(DIS_ERR_DEVICE, "search launch failed");
+        if (l > g.F && dis::launch_densify(densify_level(g, l, w.pu, w.dense), 1, s) != hipSuccess)
+            return fail(DIS_ERR_DEVICE, "densify launch failed");
     }
-    if (rc == DIS_OK) {
-        const dis::LevelGeom& LF = g.lv[g.F];
-        if (hipMemcpyAsync(outflow, dense + LF.dense_off, sizeof(float2) * LF.W * LF.H, hipMemcpyDeviceToHost,
-                           s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            rc = fail(DIS_ERR_DEVICE, "result download failed");
-    }
-    hipStreamSynchronize(s);
-    cleanup();
-    return rc;
+    // the finest level's dense flow (src/patch_grid.cpp:121-182) is the output
+    if (dis::launch_densify(densify_level(g, g.F, w.pu, w.dense), 1, s) != hipSuccess)
+        return fail(DIS_ERR_DEVICE, "densify launch failed");
+    const dis::LevelGeom& LF = g.lv[g.F];
+    if (hipMemcpyAsync(outflow, w.dense + LF.dense_off, sizeof(float2) * LF.W * LF.H, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return fail(DIS_ERR_DEVICE, "result download failed");
+    return DIS_OK;
 }
 
 dis_status dis_flow_color(const float* flow, int n, int width, int height, float maxmotion, uint8_t* bgr,

@@ -412,7 +412,12 @@ struct BlockLds {
 // is appended to the launch's fallback list (a.fb_count / a.fb_list) for
 // k_search8_fb and nothing is written here (keeps this kernel's registers
 // low enough for 4 waves per SIMD at LPP 2).
-template <int LPP, bool kFallback, bool kPaper, bool kFma = false>
+// kPhys (the compat entry dis_flow_from_pyramids, OpticalFlowClass semantics):
+// the caller's physically padded planes -- template gradients read from its
+// dx/dy planes (whatever their padding holds), I1 taps from its padded I1
+// plane clamped to the padded extent -- instead of Sobel of the level image
+// and virtual replicate padding.
+template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -432,7 +437,10 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const bool active = gx < a.npw && gy < a.nph;
     const int W = a.W, H = a.H;
     const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off;
-    const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off;
+    // I1 addressing: row stride ld, origin at image pixel (0, 0), taps clamped
+    // to [lo, W-1+pad] x [lo, H-1+pad] (virtual: the level plane, replicate)
+    const int pad = kPhys ? a.pad : 0, ld = W + 2 * pad, lo = -pad;
+    const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off + (kPhys ? pad * ld + pad : 0);
     const int irx = gx * st + a.offw, iry = gy * st + a.offh;
     const float rx = (float)irx, ry = (float)iry;
 
@@ -482,7 +490,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int x0 = bgx0 * st + a.offw - 5, y0 = bgy0 * st + a.offh - 5;
     const int RW = (bgx1 - bgx0) * st + 10, RH = (bgy1 - bgy0) * st + 10;
     const int RS = RW | 1;  // odd row stride
-    {
+    if constexpr (!kPhys) {
         // 64-column strips; rows in groups of 8 per wave: 8 loads in flight
         // per lane, bounded registers (region fits the tile buffer: host-checked)
         for (int cs = 0; cs < RW; cs += 64) {
@@ -523,7 +531,17 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     // Lane q: columns lane_col(q, ci); region column of pixel column c is
     // lx + 1 + c, its Sobel taps lx + c .. lx + c + 2.
     float gdx[8 * NC], gdy[8 * NC];
-    if (active) {
+    if (kPhys && active) {
+        // the caller's gradient planes at the patch pixels (padded coordinates)
+        const size_t o = (size_t)pair * a.plane_stride + a.plane_off + (size_t)(iry - 4 + pad) * ld + irx - 4 + pad;
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                gdx[8 * ci + j] = a.gdx_plane[o + (size_t)j * ld + lane_col<LPP>(q, ci)];
+                gdy[8 * ci + j] = a.gdy_plane[o + (size_t)j * ld + lane_col<LPP>(q, ci)];
+            }
+    } else if (active) {
         constexpr int NX = (NC == 1) ? 3 : (NC == 8) ? 10 : 6;
         const float* reg = tile + ((gy - bgy0) * st) * RS + (gx - bgx0) * st + (NC == 2 ? q : NC == 4 ? 4 * q : q);
         auto xoff = [](int m) { return NC == 2 ? 4 * (m / 3) + (m % 3) : m; };
@@ -657,13 +675,13 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         // flight, then the LDS stores)
         for (int cs = 0; cs < tw; cs += 64) {
             const int col = cs + lane;
-            const int cx = clampi(tx0 + col, 0, W - 1);
+            const int cx = clampi(tx0 + col, lo, W - 1 + pad);
             for (int r0 = wave; r0 < th; r0 += kTileGroup * NW) {
                 float v[kTileGroup];
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
                     const int r = r0 + NW * j;
-                    v[j] = (r < th && col < tw) ? I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + cx] : 0.0f;
+                    v[j] = (r < th && col < tw) ? I1[(ptrdiff_t)clampi(ty0 + r, lo, H - 1 + pad) * ld + cx] : 0.0f;
                 }
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
@@ -690,7 +708,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             iterate<LPP, true, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
                 const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
                 return [=](int k, int c) {
-                    return I1[(size_t)clampi(y0 + k, 0, H - 1) * W + clampi(x0 + c, 0, W - 1)];
+                    return I1[(ptrdiff_t)clampi(y0 + k, lo, H - 1 + pad) * ld + clampi(x0 + c, lo, W - 1 + pad)];
                 };
             });
         }
@@ -706,12 +724,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 }
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
-template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false>
+template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false, bool kPhys = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
-    search_block<LPP, kFallback, kPaper, kFma>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+    search_block<LPP, kFallback, kPaper, kFma, kPhys>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
@@ -719,7 +737,7 @@ k_search8(Search8Args a)
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
 // its workgroups cannot take the slots another stream's search kernel frees,
 // and the (usually empty) launch waited 70-150 us for that kernel to drain.
-template <int LPP, bool kPaper = false, bool kFma = false>
+template <int LPP, bool kPaper = false, bool kFma = false, bool kPhys = false>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
 __attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
@@ -730,7 +748,7 @@ k_search8_fb(Search8Args a)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int e = a.fb_list[i];
         const int bx = e % nbx, t = e / nbx;
-        search_block<LPP, true, kPaper, kFma>(a, bx, t % nby, t / nby, S);
+        search_block<LPP, true, kPaper, kFma, kPhys>(a, bx, t % nby, t / nby, S);
         __syncthreads();  // LDS reuse by the next listed block
     }
 }
@@ -798,6 +816,22 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     }
 }
 
+// compat path (physical planes): exact kernels, 2 lanes per patch (tile +
+// fallback) or 8 on small levels
+static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 grid, dim3 fb_grid, hipStream_t s)
+{
+    if (L == 2) {
+        if (split) {
+            hipLaunchKernelGGL((k_search8<2, false, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
+        } else {
+            hipLaunchKernelGGL((k_search8<2, true, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
+        }
+    } else {
+        hipLaunchKernelGGL((k_search8<8, true, false, false, true>), grid, dim3(kThreads<8>), 0, s, a);
+    }
+}
+
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t)
 {
     const int L = a.lanes_per_patch;
@@ -811,7 +845,10 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
-    if (a.paper)  // paper mode has no tolerance variant: always the exact kernels
+    if (a.gdx_plane) {  // physical planes (compat): exact, non-paper, LPP 2 or 8
+        if ((L != 2 && L != 8) || a.paper || a.fma || !a.gdy_plane || a.pad < 0) return hipErrorInvalidValue;
+        launch_search8_phys(a, L, split, grid, fb_grid, s);
+    } else if (a.paper)  // paper mode has no tolerance variant: always the exact kernels
         launch_search8_t<true, false>(a, L, split, grid, fb_grid, s, t);
     else if (a.fma)
         launch_search8_t<false, true>(a, L, split, grid, fb_grid, s, t);

@@ -90,14 +90,25 @@ def test_stage_dumps_bitexact(disflow_mod, oracle):
         _assert_bitexact(eng.debug_dump(S.STAGE_DENSE, l).reshape(ds[l].shape), ds[l], f"dense l{l}")
 
 
-def test_compat_constructor_path_bitexact(disflow_mod, oracle):
+@pytest.mark.parametrize("W,H,C,F,ps,it,ov,kind", [
+    (160, 128, 3, 1, 8, 10, 0.7, "synth"),
+    (1920, 1080, 6, 1, 8, 25, 0.625, "synth"),      # config 2 knobs: the fast kernel, 2 and 8 lanes/patch
+    (640, 480, 4, 2, 8, 12, 0.5, "unrelated"),      # spread blocks: the tile fallback on physical planes
+    (320, 240, 3, 0, 6, 8, 0.5, "synth"),           # patch size 6: the generic kernel
+])
+def test_compat_constructor_path_bitexact(disflow_mod, oracle, W, H, C, F, ps, it, ov, kind):
     # OpticalFlowClass(...) semantics over caller-built padded pyramids
-    W, H, C, F, ps, it, ov = 160, 128, 3, 1, 8, 10, 0.7
-    I0, I1 = disflow_mod.synth_pair(21, W, H)
+    # (include/optical_flow.hpp:43-54): repeated calls reuse the cached workspace
+    if kind == "unrelated":
+        I0, _ = disflow_mod.synth_pair(5, W, H)
+        I1, _ = disflow_mod.synth_pair(6, W, H)
+    else:
+        I0, I1 = disflow_mod.synth_pair(21 + W, W, H)
     Wp, Hp, P0, PX, PY, P1, _, _ = oracle.build_pyramids(I0, I1, C, ps)
     exp = oracle.flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, 1)
-    got = disflow_mod.optical_flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, True)
-    _assert_bitexact(got, exp, "compat flow")
+    for _ in range(2):
+        got = disflow_mod.optical_flow_from_pyramids(P0, PX, PY, P1, ps, Wp, Hp, C, F, it, ps, ov, True)
+        _assert_bitexact(got, exp, f"compat flow {W}x{H} ps {ps} {kind}")
 
 
 def test_batch_equals_single_and_deterministic(disflow_mod):

@@ -11,6 +11,9 @@ resident in HBM, batch per call as given, `steps` timed calls after warmup.
   2f / 3f   configs 2 / 3 with DIS_PRECISION_FMA (contracted search arithmetic,
             within the stated tolerance; tests/test_gpu_tolerance.py)
   colour    1920x1080  Middlebury colour coding of 32 flow fields (dis_flow_color)
+  compat    1920x1080  MEDIUM through the reference-interface entry (dis_flow_from_pyramids,
+            OpticalFlowClass semantics: host padded pyramids in, finest-level flow out,
+            synchronous) beside dis_calc_u8 on host frames, one pair per call
 """
 import argparse
 import json
@@ -111,15 +114,63 @@ def run_colour(steps, warmup):
             "hbm_gbs": moved / el / 1e9, "hbm_frac": moved / el / 8e12}
 
 
+def run_compat(steps, warmup):
+    W, H = 1920, 1080
+    p = disflow.preset_params(disflow.Preset.MEDIUM, W, H)
+    C, F, ps = p.coarsest_scale, p.finest_scale, p.patch_size
+    I0, I1 = disflow.synth_pair(0, W, H)
+    eng = disflow.DenseInverseSearch(p, W, H, max_batch=1)
+    eng.set_debug(True)
+    eng.calc(I0, I1)
+    # the caller's padded planes (construct_pyramide layout), from this engine's own level images
+    wl = disflow.workload(p, W, H)
+    Wp, Hp = wl["padded_width"], wl["padded_height"]
+    P1, PX, PY = [], [], []
+    for l in range(C + 1):
+        w, h = Wp >> l, Hp >> l
+        if l < F:
+            z = np.zeros((h + 2 * ps, w + 2 * ps), np.float32)
+            P1.append(z), PX.append(z), PY.append(z)
+            continue
+        P1.append(np.pad(eng.debug_dump(disflow.STAGE_IMG1, l).reshape(h, w), ps, mode="edge"))
+        PX.append(np.pad(eng.debug_dump(disflow.STAGE_DX0, l).reshape(h, w), ps))
+        PY.append(np.pad(eng.debug_dump(disflow.STAGE_DY0, l).reshape(h, w), ps))
+    eng.set_debug(False)
+
+    def compat():
+        return disflow.optical_flow_from_pyramids(P1, PX, PY, P1, ps, Wp, Hp, C, F, p.iterations, ps,
+                                                  p.patch_overlap, True)
+
+    def calc():
+        return eng.calc(I0, I1)
+    res = {}
+    for name, fn in (("compat", compat), ("calc", calc)):
+        for _ in range(warmup):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        res[name] = steps / (time.perf_counter() - t0)
+    eng.close()
+    return {"config": "compat 1920x1080 MEDIUM, one pair per call, host memory",
+            "compat_pairs_per_s": res["compat"], "calc_u8_pairs_per_s": res["calc"],
+            "compat_over_calc": res["compat"] / res["calc"],
+            "note": "compat = dis_flow_from_pyramids (H2D of the padded dx/dy/I1 planes, fast search, "
+                    "finest-level flow D2H); calc = dis_calc_u8 host mode (H2D of the u8 frames, full path, "
+                    "full-resolution flow D2H)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,2,3,5,2p,2f,3f,colour")
+    ap.add_argument("--configs", default="1,2,3,5,2p,2f,3f,colour,compat")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     for c in a.configs.split(","):
         if c == "colour":
             r = run_colour(a.steps, a.warmup)
+        elif c == "compat":
+            r = run_compat(a.steps, a.warmup)
         else:
             name, W, H, preset, B = CONFIGS[c][:5]
             steps = max(2, a.steps // (4 if c == "5" else 1))
