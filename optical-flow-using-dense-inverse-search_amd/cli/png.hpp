@@ -94,7 +94,8 @@ inline Gray decode_gray(const std::vector<uint8_t>& d, const std::string& name =
         }
         p += 12 + len;
     }
-    if (w < 1 || h < 1 || w > (1 << 16) || h > (1 << 16)) throw std::runtime_error(name + ": bad size");
+    if (w < 1 || h < 1 || w > (1 << 16) || h > (1 << 16) || (long long)w * h > (1LL << 28))
+        throw std::runtime_error(name + ": bad size");  // (the engine's frame limit, dis_create)
     if (interlace) throw std::runtime_error(name + ": interlaced PNG not supported");
     int ch;
     switch (ctype) {

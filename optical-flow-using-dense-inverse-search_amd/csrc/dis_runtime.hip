@@ -14,6 +14,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "dis_kernels.h"
 
 namespace {
@@ -296,6 +298,27 @@ int upsample_xmax(const dis::Geometry& g)
 #endif
 
 constexpr int kStageFront = 1000, kStageBack = -1000;  // other stages: the level index
+
+// roctx range around the host-side enqueue of one stage of one sub-batch
+// ("dis: level 3 sub 1"), or of a call phase: visible in rocprofv3
+// --marker-trace timelines; no cost without a tool attached.
+struct StageRange {
+    StageRange(int stage, int sub)
+    {
+        char b[48];
+        if (stage == kStageFront)
+            std::snprintf(b, sizeof b, "dis: pyramid sub %d", sub);
+        else if (stage == kStageBack)
+            std::snprintf(b, sizeof b, "dis: output sub %d", sub);
+        else
+            std::snprintf(b, sizeof b, "dis: level %d sub %d", stage, sub);
+        roctxRangePushA(b);
+    }
+    explicit StageRange(const char* what) { roctxRangePushA(what); }
+    ~StageRange() { roctxRangePop(); }
+    StageRange(const StageRange&) = delete;
+    StageRange& operator=(const StageRange&) = delete;
+};
 
 // k_densify arguments for level l of a sub-batch's workspace slice
 dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const float* img1, float2* pu,
@@ -610,6 +633,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     if (c->done_pending && !capturing) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     if (S <= 1) {
         for (int st : stages) {
+            StageRange range(st, 0);
             dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
             if (r != DIS_OK) return r;
         }
@@ -636,6 +660,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         const int st = stage_major ? stages[i / S] : stages[i % stages.size()];
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
         hipStream_t sk = k < k0 ? s : c->sub[k];
+        StageRange range(st, k);
         dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
                                  stride, pair_stride, flow + (size_t)a * fpp, sk, st,
                                  (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
@@ -666,6 +691,7 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
                      G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
                      G.variant == c->variant;
     if (!hit) {
+        StageRange range("dis: graph capture");
         hipGraph_t graph = nullptr;
         DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
         const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true);
@@ -704,7 +730,10 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         G.variant = c->variant;
     }
     if (c->done_pending) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
-    DIS_HIP(hipGraphLaunch(G.exec, s));
+    {
+        StageRange range("dis: graph launch");
+        DIS_HIP(hipGraphLaunch(G.exec, s));
+    }
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;

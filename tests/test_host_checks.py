@@ -9,6 +9,8 @@ flows bit for bit)."""
 import os
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -19,3 +21,22 @@ def test_div_pre_matches_ieee_division(tmp_path):
     out = subprocess.run([exe, "10000000"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout
     assert "0 mismatches" in out.stdout
+
+
+def test_host_code_under_asan_ubsan(tmp_path):
+    """tests/cpp/sanitize_host.cpp under -fsanitize=address,undefined
+    (-fno-sanitize-recover): the C oracle on every mode, .flo I/O with a
+    bad-file corpus, the synthetic generator, and the CLI's PNG decoder on
+    truncations, corruptions (before and past the CRC check) and random
+    well-formed images of every colour type and depth."""
+    cpp = os.path.join(ROOT, "tests", "cpp")
+    exe = str(tmp_path / "sanitize_host")
+    r = subprocess.run(["make", "-s", "-C", cpp, "sanitize", f"SAN_OUT={exe}"], capture_output=True, text=True)
+    if r.returncode != 0 and "asan" in (r.stderr + r.stdout).lower() and "cannot find" in r.stderr:
+        pytest.skip("sanitizer runtime not installed")
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    out = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 failures" in out.stdout
