@@ -218,6 +218,16 @@ void dis_oracle_pyramid(const float* img, int Wp, int Hp, int coarsest,
             for (int y = 0; y < H; ++y)
                 for (int x = 0; x < W; ++x) {
                     const float* a = p + (size_t)(2 * y) * Wq + 2 * x;
+#if defined(DIS_ORACLE_CV_SIMD_DOWN)
+                    /* tolerance variant: OpenCV >= 3.0's
+                     * ResizeAreaFastVec_SIMD_32f adds the two vertical
+                     * pairs first, (tl+bl)+(tr+br), for every column but
+                     * the W % 4 tail, which keeps the scalar order */
+                    if (x < W - W % 4) {
+                        lev[(size_t)y * W + x] = ((a[0] + a[Wq]) + (a[1] + a[Wq + 1])) * 0.25f;
+                        continue;
+                    }
+#endif
                     float s = a[0] + a[1];
                     s = s + a[Wq];
                     s = s + a[Wq + 1];

@@ -9,6 +9,8 @@ other ways (oracle/Makefile `variants`):
   seqsum  every Eigen .sum() as a plain left-to-right loop
   avxsum  Eigen's sum with 8-wide AVX packets instead of 4-wide SSE
   fma     gcc -ffp-contract=fast -mfma (FMA contraction wherever it applies)
+  cvsimd  the pyramid's 2x2 area sums in OpenCV 3.x's SIMD order, (tl+bl)+(tr+br)
+          except the W % 4 column tail (the reference's OpenCV version is unknown)
 and measures, against the reference-order oracle on the same synthetic pairs:
 the final-flow end-point error (mean, p99.9, max, share of pixels > 0.01 px),
 and, on the finest searched level with identical pyramids, the share of patches
@@ -29,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "optical-flow-using-dense-inverse-search_amd")]
 import oracle_binding as ob  # noqa: E402
 
-VARIANTS = ("seqsum", "avxsum", "fma")
+VARIANTS = ("seqsum", "avxsum", "fma", "cvsimd")
 WORKLOADS = [
     # name, W, H, preset, paper, seeds
     ("640x480 ULTRAFAST", 640, 480, "ULTRAFAST", 0, range(0, 8)),
