@@ -3,6 +3,7 @@
 // oracle (test infrastructure, oracle/dis_oracle.h). Run on a GPU box by
 // tests/test_cpp_facade.py; exits non-zero on any failure.
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -57,6 +58,18 @@ int main()
         std::vector<float> ref(flow.size());
         EXPECT(dis_oracle_calc_u8(&op, W, H, I0.data(), I1.data(), W, ref.data()) == 0, "oracle ran");
         EXPECT(bitexact(flow, ref), "DenseInverseSearch::calc bit-exact vs oracle");
+        eng.set_graphs(false);  // eager enqueue: the same bits
+        EXPECT(bitexact(eng.calc(I0, I1), ref), "eager calc bit-exact vs oracle");
+        eng.set_graphs(true);
+        eng.set_precision(DIS_PRECISION_FMA);  // tolerance mode: close, not bit-exact
+        std::vector<float> fma = eng.calc(I0, I1);
+        double se = 0.0;
+        for (size_t i = 0; i < fma.size(); i += 2)
+            se += std::sqrt((double)(fma[i] - ref[i]) * (fma[i] - ref[i]) +
+                            (double)(fma[i + 1] - ref[i + 1]) * (fma[i + 1] - ref[i + 1]));
+        EXPECT(se / (fma.size() / 2) < 1e-2, "FMA mode within a loose mean-EPE bound of the oracle");
+        eng.set_precision(DIS_PRECISION_EXACT);
+        EXPECT(bitexact(eng.calc(I0, I1), ref), "back to exact");
     }
 
     // 2) OpticalFlow::OpticalFlowClass over padded pyramids, as src/main.cpp:139-189 builds them
