@@ -125,6 +125,10 @@ static int search8_lanes(int variant, long long patches, int steps)
     return big;
 }
 
+#ifndef DIS_SAME_STREAM_SKIP
+#define DIS_SAME_STREAM_SKIP 1
+#endif
+
 struct dis_ctx {
     dis_params p;
     dis::Geometry g;
@@ -144,6 +148,11 @@ struct dis_ctx {
     // caller stream, then calc_batch on `own`) never overlap on the workspace
     hipEvent_t done = nullptr;
     bool done_pending = false;
+    hipStream_t done_stream = nullptr;  // the stream `done` was recorded on
+    // the next call must wait for `done` unless it is on that same stream
+    // (stream order already serialises it; skipping the wait packet saves the
+    // inter-call gap)
+    bool needs_wait(hipStream_t s) const { return done_pending && !(DIS_SAME_STREAM_SKIP && s == done_stream); }
     hipEvent_t join[kMaxSub] = {};
     hipEvent_t staged[kMaxSub] = {};  // sub-batch k's pyramid done (pipelined start of k+1)
     // variational refinement: its ~16 launches per fixed-point iteration per level
@@ -630,7 +639,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     std::vector<int> stages = {kStageFront};
     for (int l = c->g.C; l >= c->g.F; --l) stages.push_back(l);
     stages.push_back(kStageBack);
-    if (c->done_pending && !capturing) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
+    if (c->needs_wait(s) && !capturing) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     if (S <= 1) {
         for (int st : stages) {
             StageRange range(st, 0);
@@ -641,6 +650,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         if (capturing) return DIS_OK;
         DIS_HIP(hipEventRecord(c->done, s));
         c->done_pending = true;
+        c->done_stream = s;
         return DIS_OK;
     }
     // Every sub-batch runs on a context-owned stream forked from and joined
@@ -675,6 +685,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     if (capturing) return DIS_OK;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
+    c->done_stream = s;
     return DIS_OK;
 }
 
@@ -729,7 +740,7 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         G.precision = c->precision;
         G.variant = c->variant;
     }
-    if (c->done_pending) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
+    if (c->needs_wait(s)) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     {
         StageRange range("dis: graph launch");
         DIS_HIP(hipGraphLaunch(G.exec, s));
@@ -737,6 +748,7 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
+    c->done_stream = s;
     return DIS_OK;
 }
 
