@@ -31,12 +31,25 @@ namespace {
 #endif
 constexpr int kPyrT = DIS_PYR_THREADS;  // threads per pyramid workgroup
 
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// 16-bit lanes (lo, hi) = (byte i, byte j) of the 8 bytes {w1:w0} (v_perm_b32)
+template <int I, int J>
+__device__ __forceinline__ short2v byte_pair(unsigned w0, unsigned w1)
+{
+    constexpr unsigned sel = 0x0c000c00u | (unsigned)I | ((unsigned)J << 16);
+    return __builtin_bit_cast(short2v, __builtin_amdgcn_perm(w1, w0, sel));
+}
+
 template <int LEVELS>
 __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
 {
     constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
     constexpr int N1 = T0 / 2;
-    __shared__ uint8_t srcs[2][SS * SS];
+    // u8 staging: tile column c of row r at byte r * SR + CO + c, so the body
+    // columns 1..T0 start 4-byte aligned (dword stores) and rows are aligned
+    constexpr int CO = 3, SR = (SS + CO + 3) & ~3;
+    __shared__ __attribute__((aligned(4))) uint8_t srcs[2][SS * SR];
     __shared__ float bufs0[2][N1 * N1];
     __shared__ float bufs1[2][(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
 
@@ -58,39 +71,75 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
 
     // u8 tile with a 1-pixel halo: replicate padding to Wp x Hp (floor/ceil
-    // split) composed with Sobel's reflect-101 at the Wp x Hp border. Wave w
-    // loads rows w, w+4, ...; the row offset is wave-uniform (scalar unit), the
-    // column index is computed once per lane.
+    // split) composed with Sobel's reflect-101 at the Wp x Hp border; tile
+    // column c of row r at srcs[f][r * SR + CO + c]. Every lane computes its
+    // own row / column indices (vector unit): with wave-uniform rows the
+    // per-row index and 64-bit address arithmetic ran on the scalar unit,
+    // ~750 scalar instructions per wave, which bounded the kernel.
     {
-        // wave index made provably uniform: the row arithmetic below runs on the scalar unit
-        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        constexpr int NWV = kPyrT / 64, NR = (SS + NWV - 1) / NWV;  // rows per wave
-        const int c0 = lane, c1 = lane + 64;
-        const int xs0 = clampi(reflect101(tx - 1 + c0, a.Wp) - a.pl, 0, a.W - 1);
-        const int xs1 = clampi(reflect101(tx - 1 + min(c1, SS - 1), a.Wp) - a.pl, 0, a.W - 1);
-        uint8_t v0[2][NR], v1[2][NR];
+        constexpr int NI = 2 * SS * SS;  // bytes of both frames' tiles
+        const bool dw = T0 >= 4 && a.dword_ok && tx - a.pl >= 0 && tx - a.pl + T0 <= a.W;
+        if (dw) {
+            // body columns 1..T0 map 1:1 onto 4-byte aligned source columns:
+            // dword loads (T0/4 per row) + the two halo columns as bytes
+            constexpr int Q = T0 / 4 > 0 ? T0 / 4 : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
+            constexpr int NH = 2 * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
+            unsigned body[KB];
+            uint8_t halo[KH];
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const int r = wave + NWV * j;
-                const int ys = clampi(reflect101(ty - 1 + min(r, SS - 1), a.Hp) - a.pt, 0, a.H - 1);
-                const uint8_t* row = in + (size_t)ys * a.stride;
-                v0[f][j] = (c0 < SS) ? row[xs0] : 0;
-                v1[f][j] = (c1 < SS) ? row[xs1] : 0;
+            for (int k = 0; k < KB; ++k) {
+                const int i = min(tid + kPyrT * k, NBODY - 1);
+                const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
+                const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
+                const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+                body[k] = *reinterpret_cast<const unsigned*>(in + (size_t)ys * a.stride + (tx - a.pl) + 4 * j);
             }
-        }
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+            for (int k = 0; k < KH; ++k) {
+                const int i = min(tid + kPyrT * k, NH - 1);
+                const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
+                const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
+                const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
+                const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+                halo[k] = in[(size_t)ys * a.stride + xs];
+            }
 #pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const int r = wave + NWV * j;
-                if (r < SS) {
-                    if (c0 < SS) srcs[f][r * SS + c0] = v0[f][j];
-                    if (c1 < SS) srcs[f][r * SS + c1] = v1[f][j];
+            for (int k = 0; k < KB; ++k) {
+                const int i = tid + kPyrT * k;
+                const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
+                if (NBODY % kPyrT == 0 || i < NBODY)
+                    *reinterpret_cast<unsigned*>(&srcs[f][r * SR + CO + 1 + 4 * j]) = body[k];
+            }
+#pragma unroll
+            for (int k = 0; k < KH; ++k) {
+                const int i = tid + kPyrT * k;
+                const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
+                if (i < NH) srcs[f][r * SR + CO + c] = halo[k];
+            }
+        } else {
+            // any tile (padding columns, unaligned strides): one byte per item,
+            // 8 loads in flight per lane (bounded registers)
+            constexpr int KI = (NI + kPyrT - 1) / kPyrT, G = 8;
+#pragma unroll 1
+            for (int k0 = 0; k0 < KI; k0 += G) {
+                uint8_t v[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int i = min(tid + kPyrT * (k0 + g), NI - 1);
+                    const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
+                    const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
+                    const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
+                    const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+                    v[g] = in[(size_t)ys * a.stride + xs];
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int i = tid + kPyrT * (k0 + g);
+                    const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
+                    if (i < NI) srcs[f][r * SR + CO + c] = v[g];
                 }
             }
+        }
     }
     __syncthreads();
 
@@ -115,33 +164,69 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
         // gy = (T2 - T0) / 8 exactly (the reference's float expressions have
         // no rounding here), so gx^2 + gy^2 = N / 64 exactly for the integer
         // N = k1^2 + k2^2 < 2^21, and sqrtf(N / 64) = sqrt_cr(N) / 8.
-        int R[E0 + 2][E0], T[E0 + 2][E0];
-#pragma unroll
-        for (int r = 0; r < E0 + 2; ++r) {
-            int v[E0 + 2];
-#pragma unroll
-            for (int c = 0; c < E0 + 2; ++c) v[c] = src[(E0 * by + r) * SS + E0 * bx + c];
-#pragma unroll
-            for (int c = 0; c < E0; ++c) {
-                R[r][c] = v[c + 2] - v[c];
-                T[r][c] = 2 * v[c + 1] + v[c] + v[c + 2];
-            }
-        }
         float m[E0][E0];
+        if constexpr (E0 == 4) {
+            // packed 16-bit lanes (exact: |values| <= 1020). Per window row and
+            // column c: X = (R, T) = (v[c+2] - v[c], 2 v[c+1] + v[c] + v[c+2]);
+            // per pixel: q = (k1, k2) = (2 R1 + R0 + R2, T2 - T0) = X1 (2,0) +
+            // X0 (1,-1) + X2, and N = k1^2 + k2^2 = dot2(q, q). The 6-byte row
+            // comes in as two dwords (4-byte aligned: SR and 4 bx); (v, v)
+            // broadcast pairs by v_perm.
+            const short2v c02 = {0, 2}, cm11 = {-1, 1}, c20 = {2, 0}, c1m1 = {1, -1};
+            short2v X[6][4];
 #pragma unroll
-        for (int r = 0; r < E0; ++r)
+            for (int r = 0; r < 6; ++r) {
+                // window columns 4 bx .. 4 bx + 5 = bytes CO + 4 bx ..: the last
+                // byte of dword 4 bx, dword 4 bx + 4, the first byte of 4 bx + 8
+                const unsigned* row = reinterpret_cast<const unsigned*>(src + (E0 * by + r) * SR + E0 * bx);
+                const unsigned w0 = row[0], w1 = row[1], w2 = row[2];
+                static_assert(CO == 3, "window byte map");
+                const short2v B[6] = {byte_pair<3, 3>(w0, w1), byte_pair<4, 4>(w0, w1), byte_pair<5, 5>(w0, w1),
+                                      byte_pair<6, 6>(w0, w1), byte_pair<7, 7>(w0, w1), byte_pair<4, 4>(w1, w2)};
 #pragma unroll
-            for (int c = 0; c < E0; ++c) {
-                const int k1 = 2 * R[r + 1][c] + R[r][c] + R[r + 2][c];
-                const int k2 = T[r + 2][c] - T[r][c];
-                m[r][c] = sqrt_cr((float)(k1 * k1 + k2 * k2)) * 0.125f;
+                for (int c = 0; c < 4; ++c) X[r][c] = B[c] * cm11 + (B[c + 1] * c02 + B[c + 2]);
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const short2v q = X[r + 1][c] * c20 + (X[r][c] * c1m1 + X[r + 2][c]);
+                    int n;
+                    __asm__("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(n) : "v"(q));
+                    m[r][c] = sqrt_cr((float)n);  // 8 x the magnitude (scaled below, exactly)
+                }
+        } else {
+            int R[E0 + 2][E0], T[E0 + 2][E0];
+#pragma unroll
+            for (int r = 0; r < E0 + 2; ++r) {
+                int v[E0 + 2];
+#pragma unroll
+                for (int c = 0; c < E0 + 2; ++c) v[c] = src[(E0 * by + r) * SR + CO + E0 * bx + c];
+#pragma unroll
+                for (int c = 0; c < E0; ++c) {
+                    R[r][c] = v[c + 2] - v[c];
+                    T[r][c] = 2 * v[c + 1] + v[c] + v[c + 2];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < E0; ++r)
+#pragma unroll
+                for (int c = 0; c < E0; ++c) {
+                    const int k1 = 2 * R[r + 1][c] + R[r][c] + R[r + 2][c];
+                    const int k2 = T[r + 2][c] - T[r][c];
+                    m[r][c] = sqrt_cr((float)(k1 * k1 + k2 * k2));
+                }
+        }
+        // m holds 8 x the level-0 magnitude sqrtf(N / 64) = sqrt_cr(N) / 8:
+        // scaling by a power of two commutes with every rounding below (no
+        // underflow / overflow), so the level-1 mean ((m00+m01)+m10)+m11)*0.25
+        // of the scaled values equals that of the unscaled ones times 2^-5
         if (a.write_l0) {
             float* const p0 = planes + (size_t)ty * a.Wp + tx;  // uniform base, 32-bit lane offsets
 #pragma unroll
             for (int r = 0; r < E0; ++r)
 #pragma unroll
-                for (int c = 0; c < E0; ++c) p0[(E0 * by + r) * a.Wp + E0 * bx + c] = m[r][c];
+                for (int c = 0; c < E0; ++c) p0[(E0 * by + r) * a.Wp + E0 * bx + c] = m[r][c] * 0.125f;
         }
         float* const p1 = planes + a.off[1] + (size_t)(ty / 2) * a.w[1] + tx / 2;
 #pragma unroll
@@ -151,7 +236,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 float s = m[2 * i][2 * j] + m[2 * i][2 * j + 1];
                 s = s + m[2 * i + 1][2 * j];
                 s = s + m[2 * i + 1][2 * j + 1];
-                const float l1 = s * 0.25f;
+                const float l1 = s * 0.03125f;  // (s / 8) * 0.25, exact
                 const int y1 = B1 * by + i, x1 = B1 * bx + j;
                 buf0[y1 * N1 + x1] = l1;
                 p1[y1 * a.w[1] + x1] = l1;

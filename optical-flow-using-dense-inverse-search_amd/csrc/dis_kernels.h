@@ -127,6 +127,7 @@ struct PyramidArgs {
     int w[kMaxLevels];          // plane width per level
     int* zero;                  // nzero ints set to 0 by workgroup 0 (the searches' fallback counts)
     int nzero;
+    int dword_ok;               // I0/I1, stride and pair_stride 4-byte aligned: dword row loads
 };
 
 // Fused densify + upsample + crop (dis_frontback.hip).
