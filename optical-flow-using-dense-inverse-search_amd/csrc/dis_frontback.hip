@@ -92,7 +92,12 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
                 const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
                 const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+#ifdef DIS_EXP_PYR_NOLOAD  // experiment: no HBM reads (synthetic bytes)
+                body[k] = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
+                (void)in;
+#else
                 body[k] = *reinterpret_cast<const unsigned*>(in + (size_t)ys * a.stride + (tx - a.pl) + 4 * j);
+#endif
             }
 #pragma unroll
             for (int k = 0; k < KH; ++k) {
@@ -193,7 +198,11 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                     const short2v q = X[r + 1][c] * c20 + (X[r][c] * c1m1 + X[r + 2][c]);
                     int n;
                     __asm__("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(n) : "v"(q));
+#ifdef DIS_EXP_PYR_RAWSQRT  // experiment: uncorrected sqrt (wrong in the last bit)
+                    m[r][c] = __builtin_amdgcn_sqrtf((float)n);
+#else
                     m[r][c] = sqrt_cr((float)n);  // 8 x the magnitude (scaled below, exactly)
+#endif
                 }
         } else {
             int R[E0 + 2][E0], T[E0 + 2][E0];
@@ -239,7 +248,11 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 const float l1 = s * 0.03125f;  // (s / 8) * 0.25, exact
                 const int y1 = B1 * by + i, x1 = B1 * bx + j;
                 buf0[y1 * N1 + x1] = l1;
+#ifdef DIS_EXP_PYR_NOSTORE  // experiment: no level-1 HBM writes (kept live)
+                if (l1 < -1.0f) p1[y1 * a.w[1] + x1] = l1;
+#else
                 p1[y1 * a.w[1] + x1] = l1;
+#endif
             }
     }
 
