@@ -57,6 +57,7 @@ struct Search8Args {
     float thr_sq;             // largest float s with sqrtf(s) <= outlierthresh
     int iters, norm;
     int tile_stride;          // LDS tile row stride (search8_tile_stride(steps))
+    int quad;                 // LPP 2 patch layout: 0 = 2 x 8, 1 = 4 x 4 patches per half-wave (search8_tile_quad)
     int lanes_per_patch;      // 1, 2, 4 or 8 (k_search8<LPP>)
     const float2* dense_coarse;  // non-null: init from the coarser level's DENSE flow (variational
     long long dense_stride;      //   refinement on) instead of u_coarse; float2 per pair
@@ -156,6 +157,7 @@ hipError_t launch_sobel(const Geometry& g, int l, const float* img0, float* dx, 
                         hipStream_t s);
 hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStream_t s, Timing t = {});
 int search8_tile_stride(int steps, int lanes_per_patch);
+int search8_tile_quad(int steps, int lanes_per_patch);  // LPP 2: 4 x 4-patch half-waves (Search8Args.quad)
 bool search8_lpp1_fits(int steps);
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);

@@ -125,6 +125,9 @@ static int search8_lanes(int variant, long long patches, int steps)
     return big;
 }
 
+#ifndef DIS_QUAD_LAYOUT
+#define DIS_QUAD_LAYOUT 1  // LPP-2 4 x 4-patch half-waves where they spread the LDS banks better
+#endif
 #ifndef DIS_SAME_STREAM_SKIP
 #define DIS_SAME_STREAM_SKIP 1
 #endif
@@ -472,6 +475,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
             b.lanes_per_patch = search8_lanes(c->variant, (long long)L.npw * L.nph * n, L.steps);
             b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
+            b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, b.lanes_per_patch) : 0;
             b.fb_count = fb_count + l;
             b.fb_list = c->fb + c->fb_list_off[sub][l];
             b.paper = paper ? 1 : 0;
@@ -1320,6 +1324,7 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
             b.lanes_per_patch = search8_lanes(0, (long long)L.npw * L.nph, L.steps) == 8 ? 8 : 2;
             b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
+            b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, b.lanes_per_patch) : 0;
             b.fb_count = w.fb + l;
             b.fb_list = w.fb + fb_off;
             fb_off += (size_t)((L.npw + 7) / 8) * ((L.nph + 7) / 8);

@@ -432,8 +432,14 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int st = a.steps;
     const int bgx0 = bxi * BX, bgx1 = min(bgx0 + BX - 1, a.npw - 1);
     const int bgy0 = byi * kBY, bgy1 = min(bgy0 + kBY - 1, a.nph - 1);
-    const int gx = bgx0 + (pb >> 3);
-    const int gy = bgy0 + (pb & 7);
+    // patch (lx, ly) of the block: column-major 2 x 8 patches per half-wave,
+    // or (a.quad, LPP 2) 4 x 4 quadrants -- with tile stride 72 and an odd grid
+    // step the 32 lanes of a half-wave then read 32 distinct banks at zero flow
+    // (search8_tile_layout)
+    const int lx = (LPP == 2 && a.quad) ? 4 * ((pb >> 4) & 1) + (pb & 3) : (pb >> 3);
+    const int ly = (LPP == 2 && a.quad) ? 4 * (pb >> 5) + ((pb >> 2) & 3) : (pb & 7);
+    const int gx = bgx0 + lx;
+    const int gy = bgy0 + ly;
     const bool active = gx < a.npw && gy < a.nph;
     const int W = a.W, H = a.H;
     const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off;
@@ -753,36 +759,61 @@ k_search8_fb(Search8Args a)
     }
 }
 
-// LDS tile row stride for grid step `steps` and lane layout LPP: the
+// LDS tile row stride and (LPP 2) patch layout for grid step `steps`: the
 // patches of one 32-lane LDS group sit at (steps*S*gy + steps*gx + lane column
-// offset) floats for zero flow; pick S in [tile width + 1, kTSMax] minimising
-// the worst bank multiplicity ((a/4) mod 32, ds_read_b32 banking).
-int search8_tile_stride(int steps, int lpp)
+// offset) floats for zero flow; pick S in [tile width + 1, kTSMax] (and, for
+// LPP 2, the 2 x 8 or the 4 x 4 half-wave layout) minimising the worst bank
+// multiplicity ((a/4) mod 32, ds_read_b32 banking); ties keep 2 x 8.
+static int tile_bank_multiplicity(int steps, int lpp, int quad, int S)
+{
+    int cnt[32] = {0}, m = 0;
+    for (int l = 0; l < 32; ++l) {
+        int gx, gy, off;
+        if (lpp == 1) {  // lane = patch: gx = l / 8, gy = l % 8
+            gx = l >> 3, gy = l & 7, off = 0;
+        } else if (lpp == 2) {  // 16 patches x 2 lanes (4 columns apart)
+            const int p = l >> 1;
+            gx = quad ? (p & 3) : p >> 3, gy = quad ? (p >> 2) & 3 : p & 7, off = 4 * (l & 1);
+        } else if (lpp == 4) {  // 8 patches x 4 lanes
+            gx = 0, gy = l >> 2, off = l & 3;
+        } else {  // lpp 8: 4 patches x 8 lanes
+            gx = 0, gy = (l >> 4) * 2 + ((l >> 2) & 1), off = (l & 3) | (((l >> 3) & 1) << 2);
+        }
+        const int b = (int)(((long long)steps * S * gy + steps * gx + off) % 32);
+        m = ++cnt[b] > m ? cnt[b] : m;
+    }
+    return m;
+}
+
+static void tile_layout(int steps, int lpp, int* stride, int* quad)
 {
     const int w = lpp == 1 ? kTileW<1> : kTileW<2>, smax = lpp == 1 ? kTSMax<1> : kTSMax<2>;
-    int best = w + 1, best_m = 1 << 30;
-    for (int S = w + 1; S <= smax; ++S) {
-        int cnt[32] = {0}, m = 0;
-        for (int l = 0; l < 32; ++l) {
-            int gx, gy, off;
-            if (lpp == 1) {  // lane = patch: gx = l / 8, gy = l % 8
-                gx = l >> 3, gy = l & 7, off = 0;
-            } else if (lpp == 2) {  // 16 patches x 2 lanes (4 columns apart)
-                gx = (l >> 1) >> 3, gy = (l >> 1) & 7, off = 4 * (l & 1);
-            } else if (lpp == 4) {  // 8 patches x 4 lanes
-                gx = 0, gy = l >> 2, off = l & 3;
-            } else {  // lpp 8: 4 patches x 8 lanes
-                gx = 0, gy = (l >> 4) * 2 + ((l >> 2) & 1), off = (l & 3) | (((l >> 3) & 1) << 2);
+    int best = w + 1, best_q = 0, best_m = 1 << 30;
+    for (int q = 0; q <= (lpp == 2 ? 1 : 0); ++q)
+        for (int S = w + 1; S <= smax; ++S) {
+            const int m = tile_bank_multiplicity(steps, lpp, q, S);
+            if (m < best_m) {
+                best_m = m;
+                best = S;
+                best_q = q;
             }
-            const int b = (int)(((long long)steps * S * gy + steps * gx + off) % 32);
-            m = ++cnt[b] > m ? cnt[b] : m;
         }
-        if (m < best_m) {
-            best_m = m;
-            best = S;
-        }
-    }
-    return best;
+    *stride = best;
+    *quad = best_q;
+}
+
+int search8_tile_stride(int steps, int lpp)
+{
+    int s, q;
+    tile_layout(steps, lpp, &s, &q);
+    return s;
+}
+
+int search8_tile_quad(int steps, int lpp)
+{
+    int s, q;
+    tile_layout(steps, lpp, &s, &q);
+    return q;
 }
 
 // Whether the LPP-1 layout fits: the 16x8 block's I0 region must fit its tile buffer.
