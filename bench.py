@@ -36,6 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # rounded mul/add forbid FMA, so one lane-operation per FLOP: 157.3 / 2.
 VALU_PEAK_TFLOPS = 78.6
 FMA_PEAK_TFLOPS = 157.3  # vector f32 with FMA = 2 ops (MI355X_MICROARCH.md)
+WARMUP_FLOOR_S = 0.5  # untimed GPU work before the timed region, whatever --warmup is
 
 
 def parse():
@@ -229,9 +230,19 @@ def main():
     def step():
         eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), stream.cuda_stream)
 
+    # W warmup steps, then more untimed steps until WARMUP_FLOOR_S of GPU work
+    # has run: at small W (the driver may pass --warmup 2) the card is still
+    # ramping its clocks and a short timed region (K=5 is ~8 ms) reads low
+    t_w = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
+    extra_warmup = 0
+    while time.perf_counter() - t_w < WARMUP_FLOOR_S:
+        for _ in range(8):
+            step()
+        extra_warmup += 8
+        torch.cuda.synchronize(dev)
 
     barrier()
     torch.cuda.synchronize(dev)
@@ -250,7 +261,7 @@ def main():
         eng.set_concurrency(1)
         step()
         eng.set_kernel_timing(True)  # (re)enabling starts a fresh measurement
-        for _ in range(max(3, a.steps // 5)):
+        for _ in range(max(10, a.steps // 5)):
             step()
         torch.cuda.synchronize(dev)
         n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
@@ -321,7 +332,7 @@ def main():
             eng.set_concurrency(1)
             step()
             eng.set_kernel_timing(True)
-            for _ in range(max(3, a.steps // 5)):
+            for _ in range(max(10, a.steps // 5)):
                 step()
             torch.cuda.synchronize(dev)
             n_ff, ms_ff = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
@@ -415,6 +426,9 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_extra": {"steps": extra_warmup, "floor_s": WARMUP_FLOOR_S,
+                             "note": "untimed steps added after the W warmup steps until the floor "
+                                     "of warm-up time has elapsed (clock ramp)"},
             "ms_per_step": el / a.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
