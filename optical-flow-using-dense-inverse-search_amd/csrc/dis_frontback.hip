@@ -16,6 +16,8 @@
 #include "dis_device.h"
 #include "dis_kernels.h"
 
+#include <type_traits>
+
 namespace dis {
 
 namespace {
@@ -41,8 +43,20 @@ __device__ __forceinline__ short2v byte_pair(unsigned w0, unsigned w1)
     return __builtin_bit_cast(short2v, __builtin_amdgcn_perm(w1, w0, sel));
 }
 
+#ifdef DIS_PYR_PROF  // experiment (tools/pyr_probe.hip): per-workgroup phase clocks of wave 0
+__device__ unsigned long long* g_pyr_prof;
+#define PYR_MARK(k) \
+    do { \
+        pyr_t[k] = __builtin_readcyclecounter(); \
+    } while (0)
+#else
+#define PYR_MARK(k) \
+    do { \
+    } while (0)
+#endif
+
 template <int LEVELS>
-__global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
+__global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8))) k_pyramid(PyramidArgs a)
 {
     constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
     constexpr int N1 = T0 / 2;
@@ -61,6 +75,13 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     const int nbx = gridDim.x, nby = gridDim.y;
     const int nb = nbx * nby * gridDim.z;
     const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+#ifdef DIS_PYR_PROF
+    // clocks kept in registers and stored at the end (a store here would be
+    // waited for by the first vmcnt wait)
+    unsigned long long pyr_t[5];
+    const unsigned long long pyr_w0 = wall_clock64();
+    PYR_MARK(0);
+#endif
     const int per = nb / 8;
     const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
     // (divisions run on the vector unit: make the results provably uniform)
@@ -79,12 +100,15 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     {
         constexpr int NI = 2 * SS * SS;  // bytes of both frames' tiles
         const bool dw = T0 >= 4 && a.dword_ok && tx - a.pl >= 0 && tx - a.pl + T0 <= a.W;
-        if (dw) {
-            // body columns 1..T0 map 1:1 onto 4-byte aligned source columns:
-            // dword loads (T0/4 per row) + the two halo columns as bytes
-            constexpr int Q = T0 / 4 > 0 ? T0 / 4 : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
+        // body columns 1..T0 map 1:1 onto aligned source columns: V-byte row
+        // loads (T0/V per row; 16-byte when the frames allow it, 3 per lane for
+        // a 64 x 64 tile of both frames) + the two halo columns as bytes
+        auto stage = [&](auto vw) {
+            constexpr int V = decltype(vw)::value;
+            using VT = typename std::conditional<V == 16, uint4, unsigned>::type;
+            constexpr int Q = T0 / V > 0 ? T0 / V : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
             constexpr int NH = 2 * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
-            unsigned body[KB];
+            VT body[KB];
             uint8_t halo[KH];
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
@@ -93,10 +117,11 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
                 const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
 #ifdef DIS_EXP_PYR_NOLOAD  // experiment: no HBM reads (synthetic bytes)
-                body[k] = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
+                const unsigned sy = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
+                if constexpr (V == 16) body[k] = make_uint4(sy, sy ^ 1u, sy ^ 2u, sy ^ 3u); else body[k] = sy;
                 (void)in;
 #else
-                body[k] = *reinterpret_cast<const unsigned*>(in + (size_t)ys * a.stride + (tx - a.pl) + 4 * j);
+                body[k] = *reinterpret_cast<const VT*>(in + (size_t)ys * a.stride + (tx - a.pl) + V * j);
 #endif
             }
 #pragma unroll
@@ -108,19 +133,35 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
                 halo[k] = in[(size_t)ys * a.stride + xs];
             }
+            // unconditional stores: lanes past the end rewrite the last item
+            // (same clamped index, same value) -- a conditional store let the
+            // compiler sink the last load into the branch, after the wait for
+            // the others (two HBM round trips per workgroup)
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
-                const int i = tid + kPyrT * k;
+                const int i = min(tid + kPyrT * k, NBODY - 1);
                 const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
-                if (NBODY % kPyrT == 0 || i < NBODY)
-                    *reinterpret_cast<unsigned*>(&srcs[f][r * SR + CO + 1 + 4 * j]) = body[k];
+                unsigned* d = reinterpret_cast<unsigned*>(&srcs[f][r * SR + CO + 1 + V * j]);  // 4-byte aligned
+                if constexpr (V == 16) {
+                    d[0] = body[k].x;
+                    d[1] = body[k].y;
+                    d[2] = body[k].z;
+                    d[3] = body[k].w;
+                } else {
+                    d[0] = body[k];
+                }
             }
 #pragma unroll
             for (int k = 0; k < KH; ++k) {
-                const int i = tid + kPyrT * k;
+                const int i = min(tid + kPyrT * k, NH - 1);
                 const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
-                if (i < NH) srcs[f][r * SR + CO + c] = halo[k];
+                srcs[f][r * SR + CO + c] = halo[k];
             }
+        };
+        if (dw && T0 >= 16 && a.qword_ok) {
+            stage(std::integral_constant<int, 16>{});
+        } else if (dw) {
+            stage(std::integral_constant<int, 4>{});
         } else {
             // any tile (padding columns, unaligned strides): one byte per item,
             // 8 loads in flight per lane (bounded registers)
@@ -139,14 +180,32 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const int i = tid + kPyrT * (k0 + g);
+                    const int i = min(tid + kPyrT * (k0 + g), NI - 1);  // unconditional (see above)
                     const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
-                    if (i < NI) srcs[f][r * SR + CO + c] = v[g];
+                    srcs[f][r * SR + CO + c] = v[g];
                 }
             }
         }
     }
+    PYR_MARK(1);
     __syncthreads();
+    PYR_MARK(2);
+#ifdef DIS_EXP_PYR_LOADONLY  // experiment (pyr_probe): staging only
+    if (srcs[0][tid] == 255 && srcs[1][tid] == 254) a.img0[tid] = 1.0f;
+    PYR_MARK(3);
+    PYR_MARK(4);
+    if (tid == 0) {
+        unsigned long long* o = g_pyr_prof + (size_t)lin * 8;
+        for (int k = 0; k < 5; ++k) o[k] = pyr_t[k];
+        o[5] = wall_clock64();
+        unsigned hw, xcc;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        o[6] = ((unsigned long long)xcc << 32) | hw;
+        o[7] = pyr_w0;
+    }
+    return;
+#endif
 
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -257,6 +316,7 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
     }
 
     }
+    PYR_MARK(3);
 
     // levels 2..LEVELS from LDS for both frames at once (one barrier per
     // level), ping-pong bufs0 <-> bufs1
@@ -277,9 +337,26 @@ __global__ void __launch_bounds__(kPyrT) k_pyramid(PyramidArgs a)
             s = s + p[ns + 1];
             const float v = s * 0.25f;
             nxt[kk] = v;
+#ifdef DIS_EXP_PYR_NOSMALLSTORE  // experiment: no level >= 2 HBM writes (kept live)
+            if (v < -1.0f) pl[y * a.w[l] + x] = v;
+#else
             pl[y * a.w[l] + x] = v;
+#endif
         }
     }
+    PYR_MARK(4);
+#ifdef DIS_PYR_PROF
+    if (tid == 0) {
+        unsigned hw, xcc;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long* o = g_pyr_prof + (size_t)lin * 8;
+        for (int k = 0; k < 5; ++k) o[k] = pyr_t[k];
+        o[5] = wall_clock64();
+        o[6] = ((unsigned long long)xcc << 32) | hw;
+        o[7] = pyr_w0;
+    }
+#endif
 }
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t)

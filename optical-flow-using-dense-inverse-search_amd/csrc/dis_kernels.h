@@ -128,7 +128,8 @@ struct PyramidArgs {
     int w[kMaxLevels];          // plane width per level
     int* zero;                  // nzero ints set to 0 by workgroup 0 (the searches' fallback counts)
     int nzero;
-    int dword_ok;               // I0/I1, stride and pair_stride 4-byte aligned: dword row loads
+    int dword_ok;               // I0/I1, stride, pair_stride and pad_left 4-byte aligned: dword row loads
+    int qword_ok;               // ... and 16-byte aligned, pad_left a multiple of 16: 16-byte row loads
 };
 
 // Fused densify + upsample + crop (dis_frontback.hip).

@@ -401,7 +401,9 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.zero = fb_count;
             pa.nzero = g.C + 1;
             pa.dword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
-                            (n > 1 ? pair_stride : 0)) & 3) == 0;
+                            (n > 1 ? pair_stride : 0) | (size_t)g.pad_left) & 3) == 0;
+            pa.qword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
+                            (n > 1 ? pair_stride : 0) | (size_t)g.pad_left) & 15) == 0;
             for (int l = 0; l <= g.C; ++l) {
                 pa.off[l] = g.lv[l].plane_off;
                 pa.w[l] = g.lv[l].W;

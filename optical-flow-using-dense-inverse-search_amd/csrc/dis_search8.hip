@@ -507,8 +507,12 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int r = r0 + NW * j;
+#ifdef DIS_EXP_NOREGIONLOAD  // experiment: no HBM reads of the I0 region (wrong values)
+                    v[j] = (float)(((r * 37) ^ (c0 * 11)) & 63);
+#else
                     v[j] = (r < RH && col < RW) ? I0[(size_t)clampi(reflect101(y0 + r, H), 0, H - 1) * W + c0]
                                                 : 0.0f;
+#endif
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -687,7 +691,11 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
                     const int r = r0 + NW * j;
+#ifdef DIS_EXP_NOTILELOAD  // experiment: no HBM reads of the I1 tile (wrong values)
+                    v[j] = (float)(((r * 37) ^ (cx * 11)) & 63);
+#else
                     v[j] = (r < th && col < tw) ? I1[(ptrdiff_t)clampi(ty0 + r, lo, H - 1 + pad) * ld + cx] : 0.0f;
+#endif
                 }
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {

@@ -40,6 +40,9 @@ CASES = [
     (64, 48, 1, 0, 16, 3, 0.75, 1),       # ps 16
     (37, 29, 2, 2, 2, 3, 0.0, 1),         # ps 2, F == C
     (64, 64, 3, 0, 8, 0, 0.5, 1),         # iterations 0 (one update)
+    (1000, 200, 4, 1, 8, 6, 0.5, 1),      # pyramid dword row loads (stride, pad_left 4- not 16-byte aligned)
+    (432, 320, 4, 1, 8, 6, 0.5, 1),       # pyramid 16-byte row loads, 16 x 16 tiles
+    (420, 300, 4, 1, 8, 6, 0.5, 1),       # pad_left 6: byte row loads
 ]
 
 
