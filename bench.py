@@ -267,6 +267,29 @@ def main():
         n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
         eng.set_kernel_timing(False)
         eng.set_concurrency(a.streams if a.streams else 2)
+    # measured HBM peaks on this card (SURVEY 8d asks for a stream-copy peak
+    # beside the 8 TB/s spec): device-to-device copy and fill of 1 GiB, events
+    hbm_meas = None
+    if rank == 0:
+        nbytes = 1 << 30
+        x = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        y = torch.empty_like(x)
+        x.fill_(1.0)
+
+        def rate(fn, moved):
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            e1.synchronize()
+            return moved * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+        hbm_meas = {"copy_GBps": rate(lambda: y.copy_(x), 2 * nbytes), "fill_GBps": rate(lambda: y.fill_(2.0), nbytes),
+                    "note": "torch device copy (read+write bytes) and fill of 1 GiB, 10 reps"}
+        del x, y
     # Serving pattern: two batches in flight -- steps issued
     # alternately to two contexts on two streams (one sub-batch stream each),
     # so one batch's latency-bound coarse levels and output overlap the other's
@@ -454,6 +477,7 @@ def main():
                                  "one-stream pass after the timed region; traffic = PMC HBM bytes per "
                                  "launch of that kernel (profiles/traffic.json)"},
             "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
+            "hbm_measured_peak": hbm_meas,
             "cpu_baseline": cpu,
             "gather": gather,
             "max_epe_vs_oracle": max_epe,
