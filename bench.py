@@ -59,6 +59,8 @@ def parse():
                     help="skip the extra two-batches-in-flight measurement (reported beside, never as, value)")
     ap.add_argument("--no-tolerance-mode", action="store_true",
                     help="skip the extra DIS_PRECISION_FMA measurement (reported beside, never as, value)")
+    ap.add_argument("--warmup-floor", type=float, default=WARMUP_FLOOR_S,
+                    help="seconds of untimed steps at least (after the W warmup steps); 0 under a profiler")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per search launch (from tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -238,7 +240,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     extra_warmup = 0
-    while time.perf_counter() - t_w < WARMUP_FLOOR_S:
+    while time.perf_counter() - t_w < a.warmup_floor:
         for _ in range(8):
             step()
         extra_warmup += 8
@@ -449,7 +451,7 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "warmup_extra": {"steps": extra_warmup, "floor_s": WARMUP_FLOOR_S,
+            "warmup_extra": {"steps": extra_warmup, "floor_s": a.warmup_floor,
                              "note": "untimed steps added after the W warmup steps until the floor "
                                      "of warm-up time has elapsed (clock ramp)"},
             "ms_per_step": el / a.steps * 1e3,
