@@ -388,6 +388,9 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 
 }  // namespace
 
+#ifndef DIS_XCD_REMAP
+#define DIS_XCD_REMAP 1
+#endif
 #ifndef DIS_FB_WAVES
 #define DIS_FB_WAVES 3
 #endif
@@ -743,7 +746,22 @@ __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
+#if DIS_XCD_REMAP
+    // XCD-aware block order: the dispatcher deals linear workgroup ids
+    // round-robin to the 8 XCDs; remap so each XCD walks a contiguous run of
+    // blocks and neighbouring blocks' overlapping tiles (halo rows) are
+    // fetched once into that XCD's L2 instead of once per XCD
+    const int nbx = gridDim.x, nby = gridDim.y, nb = nbx * nby * gridDim.z;
+    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    const int per = nb / 8;
+    const int t = lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
+    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
+    const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
+    search_block<LPP, kFallback, kPaper, kFma, kPhys>(a, bx, by, bz, S);
+#else
     search_block<LPP, kFallback, kPaper, kFma, kPhys>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+#endif
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
