@@ -157,7 +157,8 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * patch_size-8 search with 8 lanes per patch on levels with few patches and 2
  * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 / 5 = the
  * patch_size-8 search with 4 / 2 / 8 / 1 lanes per patch on every level (5:
- * where the 16x8-patch block fits, grid step <= 7; else 2). All are
+ * where the 16x8-patch block fits, grid step <= 7; else 2), 6 = one wave64
+ * per patch (lane = pixel) on every exact non-paper level (else 2). All are
  * bit-identical; the switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 

@@ -120,6 +120,7 @@ static int search8_lanes(int variant, long long patches, int steps)
     if (variant == 3) return 2;
     if (variant == 4) return 8;
     if (variant == 5) return dis::search8_lpp1_fits(steps) ? 1 : 2;
+    if (variant == 6) return 64;  // one wave per patch (exact, non-paper levels)
     if (patches <= DIS_LPP8_MAX_PATCHES) return 8;
     if (patches <= DIS_LPP4_MAX_PATCHES) return 4;
     return big;
@@ -138,7 +139,7 @@ struct dis_ctx {
     int device = 0;
     int max_batch = 1;
     int debug = 0;
-    int variant = 0;  // 0 auto, 1 generic only, 2/3/4/5: patch_size-8 search with 4/2/8/1 lanes per patch
+    int variant = 0;  // 0 auto, 1 generic only, 2/3/4/5/6: patch_size-8 search with 4/2/8/1/64 lanes per patch
     int last_batch = 0;
     hipStream_t own = nullptr;
     static constexpr int kMaxSub = 8;
@@ -515,6 +516,11 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             b.iters = g.iters;
             b.norm = g.norm;
             b.fma = (c->precision == DIS_PRECISION_FMA && !paper) ? 1 : 0;
+            if (b.lanes_per_patch == 64 && (paper || b.fma)) {  // exact, non-paper only
+                b.lanes_per_patch = 2;
+                b.tile_stride = dis::search8_tile_stride(L.steps, 2);
+                b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, 2) : 0;
+            }
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
@@ -1139,7 +1145,7 @@ dis_status dis_set_precision(dis_ctx* c, int mode)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 5) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..5");
+    if (variant < 0 || variant > 6) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..6");
     c->variant = variant;
     return DIS_OK;
 }

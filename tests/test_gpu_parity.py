@@ -46,6 +46,22 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("W,H,C,F,ps,it,overlap,norm", [c for c in CASES if c[4] == 8])
+def test_wave_per_patch_bitexact(disflow_mod, oracle, W, H, C, F, ps, it, overlap, norm):
+    # the north star's mapping (k_search_wave: one wave64 per patch, lane = pixel,
+    # Eigen-order cross-lane sums) on every level, incl. ragged sizes, F == 0,
+    # no normalisation and iterations 0; paper mode falls back to 2 lanes/patch
+    I0, I1 = disflow_mod.synth_pair(W * 5 + H, W, H)
+    p = _params(disflow_mod, C, F, ps, it, overlap, norm)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    eng.set_variant(6)
+    _assert_bitexact(eng.calc(I0, I1), oracle.calc_from_params(I0, I1, p), "wave per patch")
+    p.paper_mode = 1
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    eng.set_variant(6)
+    _assert_bitexact(eng.calc(I0, I1), oracle.calc_from_params(I0, I1, p), "wave per patch, paper mode")
+
+
 @pytest.mark.parametrize("W,H,C,F,ps,it,overlap,norm", CASES)
 def test_end_to_end_bitexact(disflow_mod, oracle, W, H, C, F, ps, it, overlap, norm):
     I0, I1 = disflow_mod.synth_pair(W * 7 + H, W, H)
@@ -293,9 +309,10 @@ def test_golden_fixtures_on_gpu(disflow_mod, name):
 
 @pytest.mark.parametrize("preset", ["MEDIUM", "ULTRAFAST", "SLOW"])
 def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
-    # k_search8<LPP> for LPP 2 (variant 3), 4 (variant 2), 8 (variant 4), 1 (variant 5) and
-    # the auto per-level choice (variant 0) must all equal the oracle, on the
-    # LDS-tile path and on the global-read fallback (unrelated frames)
+    # k_search8<LPP> for LPP 2 (variant 3), 4 (variant 2), 8 (variant 4), 1 (variant 5),
+    # k_search_wave (one wave per patch, variant 6) and the auto per-level choice
+    # (variant 0) must all equal the oracle, on the LDS-tile path and on the
+    # global-read fallback (unrelated frames)
     W, H = 352, 288
     p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
     if preset == "SLOW":
@@ -307,7 +324,7 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
     exp = oracle.calc_from_params(I0, I1, p)
     exp_fb = oracle.calc_from_params(J0, J1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1")):
+    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64")):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
@@ -387,11 +404,11 @@ def test_flow_color_device_pointers(disflow_mod, oracle):
         assert np.array_equal(o[k], oracle.flow_color(f[k]))
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 6])
 def test_var_refine_path_bitexact(disflow_mod, oracle, variant):
     # variational refinement on every level (fast search with dense-flow init,
     # k_vr_* kernels) vs the oracle's restatement, a batch of 3 on 2 streams;
-    # variant 1 = the generic kernels
+    # variant 1 = the generic kernels, 6 = one wave per patch
     W, H = 320, 240
     p = disflow_mod.Params(coarsest_scale=4, finest_scale=1, patch_size=8, iterations=10, patch_overlap=0.625,
                            patch_normalization=1, var_refine_iters=3)
