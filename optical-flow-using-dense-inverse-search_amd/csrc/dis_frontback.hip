@@ -55,162 +55,159 @@ __device__ unsigned long long* g_pyr_prof;
     } while (0)
 #endif
 
+// LDS of one pyramid workgroup. u8 staging: tile column c of row r at byte
+// r * SR + CO + c, so the body columns 1..T0 start 4-byte aligned (dword
+// stores) and rows are aligned
 template <int LEVELS>
-__global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8))) k_pyramid(PyramidArgs a)
+struct PyrLds {
+    static constexpr int T0 = 1 << LEVELS, SS = T0 + 2, N1 = T0 / 2, CO = 3, SR = (SS + CO + 3) & ~3;
+    static constexpr int N2 = N1 / 2 > 0 ? N1 / 2 : 1;
+    alignas(16) uint8_t srcs[2][SS * SR];
+    float bufs0[2][N1 * N1];
+    float bufs1[2][N2 * N2];
+};
+
+// Row loads of V bytes (4 or 16) for the tile body (columns 1..T0, aligned
+// source columns) + the two halo columns as bytes, for both frames
+template <int LEVELS, int V>
+struct PyrRows {
+    static constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
+    static constexpr int Q = T0 / V > 0 ? T0 / V : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
+    static constexpr int NH = 2 * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
+    using VT = typename std::conditional<V == 16, uint4, unsigned>::type;
+    VT body[KB];
+    uint8_t halo[KH];
+};
+
+template <int LEVELS, int V>
+__device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int ty, int pair, int tid,
+                                              PyrRows<LEVELS, V>& R)
 {
-    constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
-    constexpr int N1 = T0 / 2;
-    // u8 staging: tile column c of row r at byte r * SR + CO + c, so the body
-    // columns 1..T0 start 4-byte aligned (dword stores) and rows are aligned
-    constexpr int CO = 3, SR = (SS + CO + 3) & ~3;
-    __shared__ __attribute__((aligned(4))) uint8_t srcs[2][SS * SR];
-    __shared__ float bufs0[2][N1 * N1];
-    __shared__ float bufs1[2][(N1 / 2 > 0 ? N1 / 2 : 1) * (N1 / 2 > 0 ? N1 / 2 : 1)];
-
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < a.nzero) a.zero[tid] = 0;
-    // XCD-aware tile order: the dispatcher deals linear block ids round-robin
-    // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
-    // and horizontally adjacent tiles share their 128-B rows in one L2.
-    const int nbx = gridDim.x, nby = gridDim.y;
-    const int nb = nbx * nby * gridDim.z;
-    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
-#ifdef DIS_PYR_PROF
-    // clocks kept in registers and stored at the end (a store here would be
-    // waited for by the first vmcnt wait)
-    unsigned long long pyr_t[5];
-    const unsigned long long pyr_w0 = wall_clock64();
-    PYR_MARK(0);
-#endif
-    const int per = nb / 8;
-    const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
-    // (divisions run on the vector unit: make the results provably uniform)
-    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
-    const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
-    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
-    const int tx = bx * T0, ty = by * T0;
-    const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
-
-    // u8 tile with a 1-pixel halo: replicate padding to Wp x Hp (floor/ceil
-    // split) composed with Sobel's reflect-101 at the Wp x Hp border; tile
-    // column c of row r at srcs[f][r * SR + CO + c]. Every lane computes its
-    // own row / column indices (vector unit): with wave-uniform rows the
-    // per-row index and 64-bit address arithmetic ran on the scalar unit,
-    // ~750 scalar instructions per wave, which bounded the kernel.
-    {
-        constexpr int NI = 2 * SS * SS;  // bytes of both frames' tiles
-        const bool dw = T0 >= 4 && a.dword_ok && tx - a.pl >= 0 && tx - a.pl + T0 <= a.W;
-        // body columns 1..T0 map 1:1 onto aligned source columns: V-byte row
-        // loads (T0/V per row; 16-byte when the frames allow it, 3 per lane for
-        // a 64 x 64 tile of both frames) + the two halo columns as bytes
-        auto stage = [&](auto vw) {
-            constexpr int V = decltype(vw)::value;
-            using VT = typename std::conditional<V == 16, uint4, unsigned>::type;
-            constexpr int Q = T0 / V > 0 ? T0 / V : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
-            constexpr int NH = 2 * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
-            VT body[KB];
-            uint8_t halo[KH];
+    using P = PyrRows<LEVELS, V>;
+    constexpr int SS = P::SS, Q = P::Q, T0 = P::T0;
 #pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                const int i = min(tid + kPyrT * k, NBODY - 1);
-                const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
-                const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
-                const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+    for (int k = 0; k < P::KB; ++k) {
+        const int i = min(tid + kPyrT * k, P::NBODY - 1);
+        const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
+        const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
+        const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
 #ifdef DIS_EXP_PYR_NOLOAD  // experiment: no HBM reads (synthetic bytes)
-                const unsigned sy = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
-                if constexpr (V == 16) body[k] = make_uint4(sy, sy ^ 1u, sy ^ 2u, sy ^ 3u); else body[k] = sy;
-                (void)in;
+        const unsigned sy = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
+        if constexpr (V == 16)
+            R.body[k] = make_uint4(sy, sy ^ 1u, sy ^ 2u, sy ^ 3u);
+        else
+            R.body[k] = sy;
+        (void)in;
 #else
-                body[k] = *reinterpret_cast<const VT*>(in + (size_t)ys * a.stride + (tx - a.pl) + V * j);
+        R.body[k] = *reinterpret_cast<const typename P::VT*>(in + (size_t)ys * a.stride + (tx - a.pl) + V * j);
 #endif
-            }
+    }
 #pragma unroll
-            for (int k = 0; k < KH; ++k) {
-                const int i = min(tid + kPyrT * k, NH - 1);
-                const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
+    for (int k = 0; k < P::KH; ++k) {
+        const int i = min(tid + kPyrT * k, P::NH - 1);
+        const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
+        const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
+        const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
+        const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+        R.halo[k] = in[(size_t)ys * a.stride + xs];
+    }
+}
+
+// unconditional stores: lanes past the end rewrite the last item (same
+// clamped index, same value) -- a conditional store let the compiler sink the
+// last load into the branch, after the wait for the others
+template <int LEVELS, int V>
+__device__ __forceinline__ void pyr_store_rows(PyrLds<LEVELS>& S, int tid, const PyrRows<LEVELS, V>& R)
+{
+    using P = PyrRows<LEVELS, V>;
+    using L = PyrLds<LEVELS>;
+    constexpr int SS = P::SS, Q = P::Q, T0 = P::T0;
+#pragma unroll
+    for (int k = 0; k < P::KB; ++k) {
+        const int i = min(tid + kPyrT * k, P::NBODY - 1);
+        const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
+        unsigned* d = reinterpret_cast<unsigned*>(&S.srcs[f][r * L::SR + L::CO + 1 + V * j]);  // 4-byte aligned
+        if constexpr (V == 16) {
+            d[0] = R.body[k].x;
+            d[1] = R.body[k].y;
+            d[2] = R.body[k].z;
+            d[3] = R.body[k].w;
+        } else {
+            d[0] = R.body[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < P::KH; ++k) {
+        const int i = min(tid + kPyrT * k, P::NH - 1);
+        const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
+        S.srcs[f][r * L::SR + L::CO + c] = R.halo[k];
+    }
+}
+
+// whether a tile's body columns map onto aligned source columns (row loads)
+__device__ __forceinline__ bool pyr_row_loads(const PyramidArgs& a, int T0, int tx)
+{
+    return T0 >= 4 && a.dword_ok && tx - a.pl >= 0 && tx - a.pl + T0 <= a.W;
+}
+
+// u8 tile with a 1-pixel halo: replicate padding to Wp x Hp (floor/ceil
+// split) composed with Sobel's reflect-101 at the Wp x Hp border; tile column
+// c of row r at srcs[f][r * SR + CO + c]. Every lane computes its own row /
+// column indices (vector unit): with wave-uniform rows the per-row index and
+// 64-bit address arithmetic ran on the scalar unit, ~750 scalar instructions
+// per wave, which bounded the kernel.
+template <int LEVELS>
+__device__ __forceinline__ void pyr_stage(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int tid)
+{
+    using L = PyrLds<LEVELS>;
+    constexpr int T0 = L::T0, SS = L::SS, SR = L::SR, CO = L::CO;
+    const bool dw = pyr_row_loads(a, T0, tx);
+    if (dw && T0 >= 16 && a.qword_ok) {  // 16-byte row loads (3 per lane for a 64 x 64 tile of both frames)
+        PyrRows<LEVELS, 16> R;
+        pyr_load_rows(a, tx, ty, pair, tid, R);
+        pyr_store_rows(S, tid, R);
+    } else if (dw) {
+        PyrRows<LEVELS, 4> R;
+        pyr_load_rows(a, tx, ty, pair, tid, R);
+        pyr_store_rows(S, tid, R);
+    } else {
+        // any tile (padding columns, unaligned strides): one byte per item,
+        // 8 loads in flight per lane (bounded registers)
+        constexpr int NI = 2 * SS * SS, KI = (NI + kPyrT - 1) / kPyrT, G = 8;
+#pragma unroll 1
+        for (int k0 = 0; k0 < KI; k0 += G) {
+            uint8_t v[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int i = min(tid + kPyrT * (k0 + g), NI - 1);
+                const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
                 const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
                 const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
                 const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-                halo[k] = in[(size_t)ys * a.stride + xs];
-            }
-            // unconditional stores: lanes past the end rewrite the last item
-            // (same clamped index, same value) -- a conditional store let the
-            // compiler sink the last load into the branch, after the wait for
-            // the others (two HBM round trips per workgroup)
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                const int i = min(tid + kPyrT * k, NBODY - 1);
-                const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
-                unsigned* d = reinterpret_cast<unsigned*>(&srcs[f][r * SR + CO + 1 + V * j]);  // 4-byte aligned
-                if constexpr (V == 16) {
-                    d[0] = body[k].x;
-                    d[1] = body[k].y;
-                    d[2] = body[k].z;
-                    d[3] = body[k].w;
-                } else {
-                    d[0] = body[k];
-                }
+                v[g] = in[(size_t)ys * a.stride + xs];
             }
 #pragma unroll
-            for (int k = 0; k < KH; ++k) {
-                const int i = min(tid + kPyrT * k, NH - 1);
-                const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
-                srcs[f][r * SR + CO + c] = halo[k];
-            }
-        };
-        if (dw && T0 >= 16 && a.qword_ok) {
-            stage(std::integral_constant<int, 16>{});
-        } else if (dw) {
-            stage(std::integral_constant<int, 4>{});
-        } else {
-            // any tile (padding columns, unaligned strides): one byte per item,
-            // 8 loads in flight per lane (bounded registers)
-            constexpr int KI = (NI + kPyrT - 1) / kPyrT, G = 8;
-#pragma unroll 1
-            for (int k0 = 0; k0 < KI; k0 += G) {
-                uint8_t v[G];
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const int i = min(tid + kPyrT * (k0 + g), NI - 1);
-                    const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
-                    const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
-                    const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
-                    const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-                    v[g] = in[(size_t)ys * a.stride + xs];
-                }
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const int i = min(tid + kPyrT * (k0 + g), NI - 1);  // unconditional (see above)
-                    const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
-                    srcs[f][r * SR + CO + c] = v[g];
-                }
+            for (int g = 0; g < G; ++g) {
+                const int i = min(tid + kPyrT * (k0 + g), NI - 1);  // unconditional (see pyr_store_rows)
+                const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
+                S.srcs[f][r * SR + CO + c] = v[g];
             }
         }
     }
-    PYR_MARK(1);
-    __syncthreads();
-    PYR_MARK(2);
-#ifdef DIS_EXP_PYR_LOADONLY  // experiment (pyr_probe): staging only
-    if (srcs[0][tid] == 255 && srcs[1][tid] == 254) a.img0[tid] = 1.0f;
-    PYR_MARK(3);
-    PYR_MARK(4);
-    if (tid == 0) {
-        unsigned long long* o = g_pyr_prof + (size_t)lin * 8;
-        for (int k = 0; k < 5; ++k) o[k] = pyr_t[k];
-        o[5] = wall_clock64();
-        unsigned hw, xcc;
-        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        o[6] = ((unsigned long long)xcc << 32) | hw;
-        o[7] = pyr_w0;
-    }
-    return;
-#endif
+}
 
+// Level 1 (and level 0 when requested) from the staged u8 tile, then levels
+// 2..LEVELS from LDS (a barrier per level); the caller has synchronised after
+// staging and synchronises before the LDS is reused
+template <int LEVELS>
+__device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int tid)
+{
+    using L = PyrLds<LEVELS>;
+    constexpr int T0 = L::T0, N1 = L::N1, SR = L::SR, CO = L::CO;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-    const uint8_t* src = srcs[f];
-    float* buf0 = bufs0[f];
+    const uint8_t* src = S.srcs[f];
+    float* buf0 = S.bufs0[f];
     float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
     // level 1 (and level 0 when requested). A work item is a 2x2 block of
     // level-1 pixels = a 4x4 block of level-0 magnitudes read from a 6x6 u8
@@ -316,8 +313,6 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     }
 
     }
-    PYR_MARK(3);
-
     // levels 2..LEVELS from LDS for both frames at once (one barrier per
     // level), ping-pong bufs0 <-> bufs1
 #pragma unroll
@@ -326,8 +321,8 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
         const int ns = T0 >> (l - 1), nd = ns / 2, nn = nd * nd;
         for (int k = tid; k < 2 * nn; k += kPyrT) {
             const int f = k >= nn, kk = k - f * nn;
-            const float* cur = (l & 1) ? bufs1[f] : bufs0[f];
-            float* nxt = (l & 1) ? bufs0[f] : bufs1[f];
+            const float* cur = (l & 1) ? S.bufs1[f] : S.bufs0[f];
+            float* nxt = (l & 1) ? S.bufs0[f] : S.bufs1[f];
             float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
             float* const pl = planes + a.off[l] + (size_t)(ty >> l) * a.w[l] + (tx >> l);
             const int y = kk / nd, x = kk - y * nd;
@@ -344,6 +339,47 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
 #endif
         }
     }
+}
+
+template <int LEVELS>
+__global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8))) k_pyramid(PyramidArgs a)
+{
+    __shared__ PyrLds<LEVELS> S;
+    constexpr int T0 = 1 << LEVELS;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < a.nzero) a.zero[tid] = 0;
+    // XCD-aware tile order: the dispatcher deals linear block ids round-robin
+    // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
+    // and horizontally adjacent tiles share their 128-B rows in one L2.
+    const int nbx = gridDim.x, nby = gridDim.y;
+    const int nb = nbx * nby * gridDim.z;
+    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+#ifdef DIS_PYR_PROF
+    // clocks kept in registers and stored at the end (a store here would be
+    // waited for by the first vmcnt wait)
+    unsigned long long pyr_t[5];
+    const unsigned long long pyr_w0 = wall_clock64();
+    PYR_MARK(0);
+#endif
+    const int per = nb / 8;
+    const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
+    // (divisions run on the vector unit: make the results provably uniform)
+    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
+    const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
+    const int tx = bx * T0, ty = by * T0;
+    const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
+    pyr_stage(a, S, tx, ty, pair, tid);
+    PYR_MARK(1);
+    __syncthreads();
+    PYR_MARK(2);
+#ifdef DIS_EXP_PYR_LOADONLY  // experiment (pyr_probe): staging only
+    if (S.srcs[0][tid] == 255 && S.srcs[1][tid] == 254) a.img0[tid] = 1.0f;
+    PYR_MARK(3);
+#else
+    pyr_compute(a, S, tx, ty, pair, tid);
+    PYR_MARK(3);
+#endif
     PYR_MARK(4);
 #ifdef DIS_PYR_PROF
     if (tid == 0) {
