@@ -28,9 +28,13 @@ namespace {
 // grid: (Wp / T0, Hp / T0, 2 * batch), block 256; z = pair*2 + frame.
 // LEVELS (1..6) is a template parameter so every load loop has a compile-time
 // trip count and all of a thread's loads are in flight at once.
-#ifndef DIS_PYR_THREADS
-#define DIS_PYR_THREADS 256
+#ifndef DIS_PYR_NF
+#define DIS_PYR_NF 1  // frames per pyramid workgroup (1: z = 2 * pair + frame; 2: both, measured 7 % slower)
 #endif
+#ifndef DIS_PYR_THREADS
+#define DIS_PYR_THREADS (128 * DIS_PYR_NF)
+#endif
+constexpr int kPyrNF = DIS_PYR_NF;
 constexpr int kPyrT = DIS_PYR_THREADS;  // threads per pyramid workgroup
 
 typedef short short2v __attribute__((ext_vector_type(2)));
@@ -62,9 +66,9 @@ template <int LEVELS>
 struct PyrLds {
     static constexpr int T0 = 1 << LEVELS, SS = T0 + 2, N1 = T0 / 2, CO = 3, SR = (SS + CO + 3) & ~3;
     static constexpr int N2 = N1 / 2 > 0 ? N1 / 2 : 1;
-    alignas(16) uint8_t srcs[2][SS * SR];
-    float bufs0[2][N1 * N1];
-    float bufs1[2][N2 * N2];
+    alignas(16) uint8_t srcs[kPyrNF][SS * SR];
+    float bufs0[kPyrNF][N1 * N1];
+    float bufs1[kPyrNF][N2 * N2];
 };
 
 // Row loads of V bytes (4 or 16) for the tile body (columns 1..T0, aligned
@@ -72,15 +76,15 @@ struct PyrLds {
 template <int LEVELS, int V>
 struct PyrRows {
     static constexpr int T0 = 1 << LEVELS, SS = T0 + 2;
-    static constexpr int Q = T0 / V > 0 ? T0 / V : 1, NBODY = 2 * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
-    static constexpr int NH = 2 * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
+    static constexpr int Q = T0 / V > 0 ? T0 / V : 1, NBODY = kPyrNF * SS * Q, KB = (NBODY + kPyrT - 1) / kPyrT;
+    static constexpr int NH = kPyrNF * SS * 2, KH = (NH + kPyrT - 1) / kPyrT;
     using VT = typename std::conditional<V == 16, uint4, unsigned>::type;
     VT body[KB];
     uint8_t halo[KH];
 };
 
 template <int LEVELS, int V>
-__device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int ty, int pair, int tid,
+__device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int ty, int pair, int fsel, int tid,
                                               PyrRows<LEVELS, V>& R)
 {
     using P = PyrRows<LEVELS, V>;
@@ -90,7 +94,7 @@ __device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int 
         const int i = min(tid + kPyrT * k, P::NBODY - 1);
         const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
         const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
-        const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+        const uint8_t* in = ((f | fsel) ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
 #ifdef DIS_EXP_PYR_NOLOAD  // experiment: no HBM reads (synthetic bytes)
         const unsigned sy = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
         if constexpr (V == 16)
@@ -108,7 +112,7 @@ __device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int 
         const int f = i >= 2 * SS, rem = i - f * 2 * SS, r = rem >> 1, c = (rem & 1) ? T0 + 1 : 0;
         const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
         const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
-        const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+        const uint8_t* in = ((f | fsel) ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
         R.halo[k] = in[(size_t)ys * a.stride + xs];
     }
 }
@@ -157,23 +161,23 @@ __device__ __forceinline__ bool pyr_row_loads(const PyramidArgs& a, int T0, int 
 // 64-bit address arithmetic ran on the scalar unit, ~750 scalar instructions
 // per wave, which bounded the kernel.
 template <int LEVELS>
-__device__ __forceinline__ void pyr_stage(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int tid)
+__device__ __forceinline__ void pyr_stage(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int fsel, int tid)
 {
     using L = PyrLds<LEVELS>;
     constexpr int T0 = L::T0, SS = L::SS, SR = L::SR, CO = L::CO;
     const bool dw = pyr_row_loads(a, T0, tx);
     if (dw && T0 >= 16 && a.qword_ok) {  // 16-byte row loads (3 per lane for a 64 x 64 tile of both frames)
         PyrRows<LEVELS, 16> R;
-        pyr_load_rows(a, tx, ty, pair, tid, R);
+        pyr_load_rows(a, tx, ty, pair, fsel, tid, R);
         pyr_store_rows(S, tid, R);
     } else if (dw) {
         PyrRows<LEVELS, 4> R;
-        pyr_load_rows(a, tx, ty, pair, tid, R);
+        pyr_load_rows(a, tx, ty, pair, fsel, tid, R);
         pyr_store_rows(S, tid, R);
     } else {
         // any tile (padding columns, unaligned strides): one byte per item,
         // 8 loads in flight per lane (bounded registers)
-        constexpr int NI = 2 * SS * SS, KI = (NI + kPyrT - 1) / kPyrT, G = 8;
+        constexpr int NI = kPyrNF * SS * SS, KI = (NI + kPyrT - 1) / kPyrT, G = 8;
 #pragma unroll 1
         for (int k0 = 0; k0 < KI; k0 += G) {
             uint8_t v[G];
@@ -183,7 +187,7 @@ __device__ __forceinline__ void pyr_stage(const PyramidArgs& a, PyrLds<LEVELS>& 
                 const int f = i >= SS * SS, rem = i - f * SS * SS, r = rem / SS, c = rem - r * SS;
                 const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
                 const int xs = clampi(reflect101(tx - 1 + c, a.Wp) - a.pl, 0, a.W - 1);
-                const uint8_t* in = (f ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
+                const uint8_t* in = ((f | fsel) ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
                 v[g] = in[(size_t)ys * a.stride + xs];
             }
 #pragma unroll
@@ -200,15 +204,15 @@ __device__ __forceinline__ void pyr_stage(const PyramidArgs& a, PyrLds<LEVELS>& 
 // 2..LEVELS from LDS (a barrier per level); the caller has synchronised after
 // staging and synchronises before the LDS is reused
 template <int LEVELS>
-__device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int tid)
+__device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>& S, int tx, int ty, int pair, int fsel, int tid)
 {
     using L = PyrLds<LEVELS>;
     constexpr int T0 = L::T0, N1 = L::N1, SR = L::SR, CO = L::CO;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < kPyrNF; ++f) {
     const uint8_t* src = S.srcs[f];
     float* buf0 = S.bufs0[f];
-    float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+    float* planes = ((f | fsel) ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
     // level 1 (and level 0 when requested). A work item is a 2x2 block of
     // level-1 pixels = a 4x4 block of level-0 magnitudes read from a 6x6 u8
     // window; the separable Sobel row sums R/S are shared by the 16 pixels.
@@ -319,11 +323,11 @@ __device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>
     for (int l = 2; l <= LEVELS; ++l) {
         __syncthreads();
         const int ns = T0 >> (l - 1), nd = ns / 2, nn = nd * nd;
-        for (int k = tid; k < 2 * nn; k += kPyrT) {
+        for (int k = tid; k < kPyrNF * nn; k += kPyrT) {
             const int f = k >= nn, kk = k - f * nn;
             const float* cur = (l & 1) ? S.bufs1[f] : S.bufs0[f];
             float* nxt = (l & 1) ? S.bufs0[f] : S.bufs1[f];
-            float* planes = (f ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+            float* planes = ((f | fsel) ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
             float* const pl = planes + a.off[l] + (size_t)(ty >> l) * a.w[l] + (tx >> l);
             const int y = kk / nd, x = kk - y * nd;
             const float* p = cur + (2 * y) * ns + 2 * x;
@@ -368,8 +372,10 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
     const int tx = bx * T0, ty = by * T0;
-    const int pair = bz;  // both frames of the tile in one workgroup (2x the loads in flight)
-    pyr_stage(a, S, tx, ty, pair, tid);
+    // both frames of the tile in one workgroup (2x the loads in flight), or
+    // (kPyrNF 1) z = 2 * pair + frame
+    const int pair = kPyrNF == 2 ? bz : bz >> 1, fsel = kPyrNF == 2 ? 0 : bz & 1;
+    pyr_stage(a, S, tx, ty, pair, fsel, tid);
     PYR_MARK(1);
     __syncthreads();
     PYR_MARK(2);
@@ -377,7 +383,7 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     if (S.srcs[0][tid] == 255 && S.srcs[1][tid] == 254) a.img0[tid] = 1.0f;
     PYR_MARK(3);
 #else
-    pyr_compute(a, S, tx, ty, pair, tid);
+    pyr_compute(a, S, tx, ty, pair, fsel, tid);
     PYR_MARK(3);
 #endif
     PYR_MARK(4);
@@ -399,7 +405,7 @@ hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing
 {
     const int T0 = 1 << a.levels;
     if (a.levels < 1 || a.levels > 6 || a.Wp % T0 || a.Hp % T0) return hipErrorInvalidValue;
-    dim3 grid(a.Wp / T0, a.Hp / T0, batch);
+    dim3 grid(a.Wp / T0, a.Hp / T0, batch * (2 / kPyrNF));
     switch (a.levels) {
         case 1: DIS_LAUNCH(t, k_pyramid<1>, grid, dim3(kPyrT), 0, s, a); break;
         case 2: DIS_LAUNCH(t, k_pyramid<2>, grid, dim3(kPyrT), 0, s, a); break;
