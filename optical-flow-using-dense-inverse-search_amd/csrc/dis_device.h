@@ -135,4 +135,22 @@ __device__ __forceinline__ float sqrt_cr(float x)
     return y;
 }
 
+// Correctly rounded a / b for a divisor b used many times (the search's
+// per-patch LU pivots, the output kernel's densify weights), given r = RN(1 / b)
+// (one full division per patch instead of one per update): q0 = a*r is
+// within 2 ulp, one fma correction makes it faithful, and Markstein's step
+// (exact remainder e = a - b*q1, then RN(q1 + e*r)) rounds it correctly
+// (Markstein 1990; Muller et al., Handbook of FP Arithmetic, thm. 4.12),
+// given no over/underflow in the remainders -- the patch sums here are
+// image-scale. a = +-0 keeps q0 (the fma steps would turn -0 into +0);
+// b = 0 gives r = inf and NaN instead of +-inf, which the outlier test
+// resets exactly like the reference's inf.
+__device__ __forceinline__ float div_pre(float a, float b, float r)
+{
+    const float q0 = a * r;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
+    const float q2 = __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
+    return a == 0.0f ? q0 : q2;
+}
+
 }  // namespace dis

@@ -439,7 +439,9 @@ template <bool UPS, int K>
 struct OutPatch {
     static constexpr int st = (8 + K - 1) / K;
     static constexpr int PX = (OutShape<UPS>::SW + 7) / st + 2;
-    static constexpr int PY = (OutShape<UPS>::SH + 7) / st + 2;
+    // odd stride (in float2): the densify's lanes read patches at different
+    // column offsets xr.x, which an even stride maps onto the same LDS banks
+    static constexpr int PY = ((OutShape<UPS>::SH + 7) / st + 2) | 1;
 };
 
 // cv::resize INTER_LINEAR source index / fraction for destination index d at
@@ -461,6 +463,63 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
     *f = fx;
 }
 
+
+// one float4 (two output pixels) of the flow; streaming store by default: the
+// flow is not read back on the device, so it should not displace the level
+// planes and frames the next call's kernels read from L2 / MALL
+__device__ __forceinline__ void store_flow2(float2* dst, float2 o0, float2 o1)
+{
+#ifdef DIS_OUT_NO_NT
+    *reinterpret_cast<float4*>(dst) = make_float4(o0.x, o0.y, o1.x, o1.y);
+#else
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((f4v){o0.x, o0.y, o1.x, o1.y}, reinterpret_cast<f4v*>(dst));
+#endif
+}
+
+// Output rows of an interior tile at F == 1 (every tap unclamped, every column
+// two-tap, the tile inside W x H). lin_coef then reduces to
+// i = (d - 1) >> 1, f = 0.75 (d even) / 0.25 (d odd) for a destination index d,
+// so with the thread's rows and columns starting at even y / x the taps are
+// static given the parities YP = (pad_top - 1) & 1, XP = (pad_left - 1) & 1,
+// and each source row's horizontal interpolation -- the same expression as
+// the general path, hence the same value -- is formed once and shared by the
+// (up to four) output rows that read it.
+template <int YP, int XP, int SW, int RPT>
+__device__ __forceinline__ void out_rows_f1(const OutputArgs& a, const float2* dense, int i0, int j0, int px, int py,
+                                            int pair)
+{
+    constexpr int LP = XP ^ 1;                               // pad_left & 1 = parity of x = px + pad_left
+    constexpr float xf0 = LP ? 0.25f : 0.75f, xf1 = LP ? 0.75f : 0.25f;
+    constexpr int o1 = LP ? 0 : 1;                           // source column of pixel 1 - that of pixel 0
+    constexpr int NR = (RPT - 1 + YP) / 2 + 2;               // source rows of the thread's RPT output rows
+    const int c0 = ((px + a.pad_left - 1) >> 1) - i0;
+    const int rs = ((py + a.pad_top - 1) >> 1) - j0;
+    float2 h0[NR], h1[NR];
+#pragma unroll
+    for (int t = 0; t < NR; ++t) {
+        const float2* row = dense + (rs + t) * SW + c0;
+        const float2 sa = row[0], sb = row[1];
+        h0[t] = make_float2(sa.x * (1.f - xf0) + sb.x * xf0, sa.y * (1.f - xf0) + sb.y * xf0);
+        if constexpr (o1) {
+            const float2 sc = row[2];
+            h1[t] = make_float2(sb.x * (1.f - xf1) + sc.x * xf1, sb.y * (1.f - xf1) + sc.y * xf1);
+        } else {
+            h1[t] = make_float2(sa.x * (1.f - xf1) + sb.x * xf1, sa.y * (1.f - xf1) + sb.y * xf1);
+        }
+    }
+    float2* dst = a.flow + (size_t)pair * a.W * a.H + (size_t)py * a.W + px;
+#pragma unroll
+    for (int d = 0; d < RPT; ++d) {
+        const int t = (d + YP) >> 1;                         // yi - (first source row)
+        const float yf = ((d + YP) & 1) ? 0.75f : 0.25f;     // y + pad_top even -> 0.75
+        const float b0 = 1.f - yf, b1 = yf;
+        const float2 o0 = make_float2(h0[t].x * b0 + h0[t + 1].x * b1, h0[t].y * b0 + h0[t + 1].y * b1);
+        const float2 oo = make_float2(h1[t].x * b0 + h1[t + 1].x * b1, h1[t].y * b0 + h1[t + 1].y * b1);
+        store_flow2(dst + (size_t)d * a.W, o0, oo);
+    }
+}
+
 }  // namespace
 
 // grid (ceil(W/64), ceil(H/16), batch), block 256 (2x2 output pixels per thread).
@@ -474,7 +533,8 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
     constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
     constexpr int kOutPX = OutPatch<UPSAMPLE, K>::PX, kOutPY = OutPatch<UPSAMPLE, K>::PY;
-    __shared__ float2 pu[kOutPX * kOutPY];
+    __shared__ float2 pu[(kOutPX + K + 2) * kOutPY];  // + the padding the unmasked taps may read
+    __shared__ float rtab[K * K + 1];                  // RN(1 / (0.5 n)), n covering patches
     __shared__ float2 dense[kOutSW * kOutSH];
     __shared__ int2 cr[kOutSW], rr[kOutSH];
     const int tid = threadIdx.x;
@@ -520,6 +580,10 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             if (tid + 256 * j < kOutPX * kOutPY)
                 pu[tid + 256 * j] = kPaper ? v[j] : make_float2(v[j].x * 0.5f, v[j].y * 0.5f);
     }
+    if (!kPaper && tid >= 64 && tid - 64 <= K * K) {
+        const int n = tid - 64;
+        rtab[n] = n ? 1.0f / (0.5f * (float)n) : 0.0f;
+    }
     // covering patch ranges per window column / row (one floordiv pair each)
     if (tid < rw) {
         const int px = i0 + tid;
@@ -533,8 +597,15 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     }
     __syncthreads();
     const float sc = a.sc;
+    const float rrw = __builtin_amdgcn_rcpf((float)rw);  // k / rw by floordiv_r: exact for k < 2^12
     for (int k = tid; k < rw * rh; k += 256) {
-        const int r = k / rw, c = k - r * rw;
+        const int r = floordiv_r(k, rrw), c = k - r * rw;
+#ifdef DIS_EXP_OUT_NODENSE  // experiment: no densify arithmetic (wrong values)
+        if (true) {
+            dense[r * kOutSW + c] = pu[k % (kOutPX * kOutPY)];
+            continue;
+        }
+#endif
         // dense value: contributions in patch-id order, f from +0; masked
         // terms add +0, an exact no-op (f is never -0)
         const int2 xr = cr[c], yr = rr[r];
@@ -560,16 +631,32 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                     }
                 }
         } else {
+            // covering patches per axis (<= K), read at constant offsets from the
+            // first one (the LDS array is padded for the taps past the range)
+            const int nx = max(xr.y - xr.x + 1, 0), ny = max(yr.y - yr.x + 1, 0);
+            const float2* pb = pu + xr.x * kOutPY + yr.x;
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                    const bool ok = (xr.x + i <= xr.y) && (yr.x + j <= yr.y);
-                    const float2 t = pu[ok ? (xr.x + i) * kOutPY + yr.x + j : 0];
+                    const bool ok = i < nx && j < ny;
+                    const float2 t = pb[i * kOutPY + j];
                     fx = fx + (ok ? t.x : 0.0f);
                     fy = fy + (ok ? t.y : 0.0f);
-                    w = w + (ok ? 0.5f : 0.0f);
                 }
+            // the reference's weight sum of 0.5 per covering patch, exactly
+            const int n = nx * ny;
+            w = 0.5f * (float)n;
+            // fx / w correctly rounded from the tabulated RN(1 / w) (div_pre);
+            // tiny nonzero numerators, whose remainders could underflow, take
+            // the IEEE division below
+            const bool tiny = (fx != 0.0f && fabsf(fx) < 0x1p-100f) || (fy != 0.0f && fabsf(fy) < 0x1p-100f);
+            if (n > 0 && !tiny) {
+                const float rcp = rtab[n];
+                fx = div_pre(fx, w, rcp);
+                fy = div_pre(fy, w, rcp);
+                w = 0.0f;  // done
+            }
         }
         if (w > 0) {
             fx = fx / w;
@@ -582,11 +669,34 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 
     constexpr int RPT = kOutTH / 8;  // output rows per thread
     const int px = ox + (tid & 31) * 2, py = oy + (tid >> 5) * RPT;
+#ifndef DIS_EXP_OUT_NOUPS
+    if constexpr (UPSAMPLE) {
+        const int xh = ox + kOutTW - 1 + a.pad_left, yh = oy + kOutTH - 1 + a.pad_top;
+        if (a.F == 1 && a.vec_store && ox + kOutTW <= a.W && oy + kOutTH <= a.H && ox + a.pad_left >= 1 &&
+            oy + a.pad_top >= 1 && ((xh - 1) >> 1) + 1 <= a.wF - 1 && ((yh - 1) >> 1) + 1 <= a.hF - 1 &&
+            xh < a.xmax) {  // uniform: an interior tile
+            switch (((a.pad_top - 1) & 1) * 2 + ((a.pad_left - 1) & 1)) {
+                case 0: out_rows_f1<0, 0, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
+                case 1: out_rows_f1<0, 1, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
+                case 2: out_rows_f1<1, 0, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
+                default: out_rows_f1<1, 1, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
+            }
+            return;
+        }
+    }
+#endif
 #pragma unroll
     for (int dy = 0; dy < RPT; ++dy) {
         const int y = py + dy;
         if (y >= a.H) continue;
         float2 o[2];
+#ifdef DIS_EXP_OUT_NOUPS  // experiment: no interpolation arithmetic (wrong values)
+        if (true) {
+            const float2* row = dense + ((y - oy) >> 1) * kOutSW + ((px - ox) >> 1);
+            o[0] = row[0];
+            o[1] = row[1];
+        } else
+#endif
         if (UPSAMPLE) {
             int yi;
             float yf;
@@ -624,9 +734,9 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         }
         float2* dst = a.flow + (size_t)pair * a.W * a.H + (size_t)y * a.W + px;
         if (px + 1 < a.W) {
-            if (a.vec_store)
-                *reinterpret_cast<float4*>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
-            else {
+            if (a.vec_store) {
+                store_flow2(dst, o[0], o[1]);
+            } else {
                 dst[0] = o[0];
                 dst[1] = o[1];
             }

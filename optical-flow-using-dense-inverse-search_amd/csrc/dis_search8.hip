@@ -214,23 +214,6 @@ __device__ __forceinline__ float patch_dot(const float (&g)[8 * kNCol<LPP>], Fn&
     }
 }
 
-// Correctly rounded a / b for the per-patch LU pivots b, given r = RN(1 / b)
-// (one full division per patch instead of one per update): q0 = a*r is
-// within 2 ulp, one fma correction makes it faithful, and Markstein's step
-// (exact remainder e = a - b*q1, then RN(q1 + e*r)) rounds it correctly
-// (Markstein 1990; Muller et al., Handbook of FP Arithmetic, thm. 4.12),
-// given no over/underflow in the remainders -- the patch sums here are
-// image-scale. a = +-0 keeps q0 (the fma steps would turn -0 into +0);
-// b = 0 gives r = inf and NaN instead of +-inf, which the outlier test
-// resets exactly like the reference's inf.
-__device__ __forceinline__ float div_pre(float a, float b, float r)
-{
-    const float q0 = a * r;
-    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
-    const float q2 = __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
-    return a == 0.0f ? q0 : q2;
-}
-
 // Wave-wide min/max of an int (all 64 lanes participate).
 __device__ __forceinline__ int wave_min(int v)
 {

@@ -72,6 +72,17 @@ def test_end_to_end_bitexact(disflow_mod, oracle, W, H, C, F, ps, it, overlap, n
     _assert_bitexact(got, exp, f"flow {W}x{H}")
 
 
+@pytest.mark.parametrize("W,H", [(998, 202), (1000, 202), (998, 200), (1000, 200), (259, 197)])
+def test_output_interior_tiles_every_pad_parity(disflow_mod, oracle, W, H):
+    # k_output's interior-tile path at F == 1 specialises on the parities of
+    # pad_top and pad_left (odd / even padding of Wp x Hp) -- all four, plus
+    # the border tiles of the general path around them
+    I0, I1 = disflow_mod.synth_pair(W + 3 * H, W, H)
+    p = _params(disflow_mod, 4, 1, 8, 8, 0.625)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    _assert_bitexact(eng.calc(I0, I1), oracle.calc_from_params(I0, I1, p), f"flow {W}x{H}")
+
+
 def test_large_shift_outliers_bitexact(disflow_mod, oracle):
     # big translation: many patches hit the outlier reset / OOB start (Q4, Q5)
     I0, I1 = helpers.shifted_pair(11, 120, 160, dx=9.5, dy=-7.25)

@@ -4,7 +4,9 @@
  * r = RN(1/b); a = +-0 keeps q0. Random a, b with exponents in [-60, 60]
  * (the patch sums and LU pivots of 8-bit images) and mantissas biased to the
  * edge cases (all ones, zero). Usage: div_check [samples]; exit 1 on a
- * mismatch. Build: gcc -O2 -mfma -ffp-contract=off div_check.c -lm */
+ * mismatch. A second pass checks the output kernel's densify divisors
+ * b = n / 2 (n = 1..16 covering patches) against numerators of exponent
+ * [-100, 60] (k_output sends |a| < 2^-100 to IEEE division). Build: gcc -O2 -mfma -ffp-contract=off div_check.c -lm */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -44,6 +46,20 @@ int main(int argc, char** argv)
             bad++;
         }
     }
-    printf("div_check: %ld samples, %ld mismatches\n", n, bad);
+    for (long i = 0; i < n / 4; i++) {  /* densify weights */
+        const uint64_t x = rnd();
+        const int nc = 1 + (int)(x % 16);
+        const uint32_t ea = (uint32_t)(27 + ((x >> 8) % 161));
+        uint32_t ma = (uint32_t)(x >> 16) & 0x7fffff;
+        if ((x >> 62) & 1) ma = (i & 4) ? 0x7fffff : ma;
+        const float a = bf(((uint32_t)(x >> 39 & 1) << 31) | ea << 23 | ma);
+        volatile float bv = 0.5f * (float)nc, av = a;
+        const float r = 1.0f / bv, ref = av / bv, got = div_pre(a, bv, r);
+        if (fb(got) != fb(ref)) {
+            if (bad < 10) printf("a=%a b=%a ref=%a got=%a\n", a, (float)bv, ref, got);
+            bad++;
+        }
+    }
+    printf("div_check: %ld + %ld samples, %ld mismatches\n", n, n / 4, bad);
     return bad != 0;
 }
