@@ -464,16 +464,17 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 }
 
 
-// one float4 (two output pixels) of the flow; streaming store by default: the
-// flow is not read back on the device, so it should not displace the level
-// planes and frames the next call's kernels read from L2 / MALL
+// one float4 (two output pixels) of the flow. DIS_OUT_NT: streaming
+// (non-temporal) stores -- the one-stream kernel trace gets faster (the next
+// call's k_pyramid 122 -> 112 us: the flow no longer displaces its frames in
+// L2 / MALL), but the two-sub-batch step measured 2-3 % slower
 __device__ __forceinline__ void store_flow2(float2* dst, float2 o0, float2 o1)
 {
-#ifdef DIS_OUT_NO_NT
-    *reinterpret_cast<float4*>(dst) = make_float4(o0.x, o0.y, o1.x, o1.y);
-#else
+#ifdef DIS_OUT_NT
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((f4v){o0.x, o0.y, o1.x, o1.y}, reinterpret_cast<f4v*>(dst));
+#else
+    *reinterpret_cast<float4*>(dst) = make_float4(o0.x, o0.y, o1.x, o1.y);
 #endif
 }
 
