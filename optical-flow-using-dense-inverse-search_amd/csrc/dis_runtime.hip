@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 
 #include "dis_kernels.h"
 
@@ -168,17 +168,26 @@ struct dis_ctx {
     } vrg[kMaxSub][dis::kMaxLevels];
     hipStream_t cap = nullptr;  // capture-only stream
     // The whole batch call (both sub-batches' pyramid, level searches and
-    // output, with the fork/join) replayed as one HIP graph, captured on the
-    // first call with a given key and re-captured (exec updated in place) when
-    // the key changes: dis_set_graphs, default on.
+    // output, with the fork/join) replayed as one HIP graph: dis_set_graphs,
+    // default on. A small LRU of executable graphs keyed by the call (buffers,
+    // batch size, sub-batches, precision, variant): a caller that ping-pongs
+    // a few buffer sets replays without re-capturing. A miss re-captures into
+    // the least recently used slot and updates its exec in place -- only after
+    // that exec's last replay has finished (`last`): the update rewrites the
+    // kernel arguments an unstarted node of that replay would still read.
     int graphs = 1;
+    static constexpr int kGraphCache = 4;
     struct MainGraph {
         hipGraphExec_t exec = nullptr;
+        hipEvent_t last = nullptr;  // recorded after this exec's latest launch
+        bool launched = false;
+        unsigned long long used = 0;  // LRU clock
         int n = -1, nsub = -1, precision = -1, variant = -1;
         const void *i0 = nullptr, *i1 = nullptr;
         void* flow = nullptr;
         size_t stride = 0, pair_stride = 0;
-    } mg;
+    } mg[kGraphCache];
+    unsigned long long graph_clock = 0;
     // workspace (device)
     float* img0 = nullptr;
     float* img1 = nullptr;
@@ -312,9 +321,30 @@ int upsample_xmax(const dis::Geometry& g)
 
 constexpr int kStageFront = 1000, kStageBack = -1000;  // other stages: the level index
 
+// roctx markers, resolved at first use with dlopen (no link-time dependency:
+// without the roctx library, or without a tool attached, they are no-ops).
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx()
+    {
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+        pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+const Roctx& roctx()
+{
+    static const Roctx r;
+    return r;
+}
+
 // roctx range around the host-side enqueue of one stage of one sub-batch
 // ("dis: level 3 sub 1"), or of a call phase: visible in rocprofv3
-// --marker-trace timelines; no cost without a tool attached.
+// --marker-trace timelines.
 struct StageRange {
     StageRange(int stage, int sub)
     {
@@ -325,13 +355,32 @@ struct StageRange {
             std::snprintf(b, sizeof b, "dis: output sub %d", sub);
         else
             std::snprintf(b, sizeof b, "dis: level %d sub %d", stage, sub);
-        roctxRangePushA(b);
+        if (roctx().push) roctx().push(b);
     }
-    explicit StageRange(const char* what) { roctxRangePushA(what); }
-    ~StageRange() { roctxRangePop(); }
+    explicit StageRange(const char* what)
+    {
+        if (roctx().push) roctx().push(what);
+    }
+    ~StageRange()
+    {
+        if (roctx().pop) roctx().pop();
+    }
     StageRange(const StageRange&) = delete;
     StageRange& operator=(const StageRange&) = delete;
 };
+
+// One mutex per device guards the device's pooled sub-batch streams
+// (sub_streams): held across a context's eager enqueue of a forked batch call
+// and across a graph capture (which puts the pooled streams into capture
+// mode), so concurrent contexts on different host threads never interleave
+// work on a shared stream while it is being captured.
+std::mutex& pool_mutex(int device)
+{
+    static std::mutex mu;
+    static std::map<int, std::mutex> per_device;
+    std::lock_guard<std::mutex> lock(mu);
+    return per_device[device];
+}
 
 // k_densify arguments for level l of a sub-batch's workspace slice
 dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const float* img1, float2* pu,
@@ -709,56 +758,86 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
 dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                              size_t pair_stride, float2* flow, hipStream_t s)
 {
-    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap)
+    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap) {
+        std::lock_guard<std::mutex> lock(pool_mutex(c->device));  // eager enqueue onto the pooled streams
         return run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
-    auto& G = c->mg;
-    const bool hit = G.exec && G.n == n && G.i0 == I0 && G.i1 == I1 && G.flow == flow && G.stride == stride &&
-                     G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
-                     G.variant == c->variant;
-    if (!hit) {
+    }
+    auto key_is = [&](const dis_ctx::MainGraph& G) {
+        return G.exec && G.n == n && G.i0 == I0 && G.i1 == I1 && G.flow == flow && G.stride == stride &&
+               G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
+               G.variant == c->variant;
+    };
+    dis_ctx::MainGraph* G = nullptr;
+    for (auto& e : c->mg)
+        if (key_is(e)) G = &e;
+    if (!G) {
+        // victim: an empty slot, else the least recently used exec
+        G = &c->mg[0];
+        for (auto& e : c->mg) {
+            if (!e.exec) {
+                G = &e;
+                break;
+            }
+            if (e.used < G->used) G = &e;
+        }
+        if (G->launched) {  // its last replay may still be in flight: never update under it
+            DIS_HIP(hipEventSynchronize(G->last));
+            G->launched = false;
+        }
+        if (!G->last) DIS_HIP(hipEventCreateWithFlags(&G->last, hipEventDisableTiming));
         StageRange range("dis: graph capture");
         hipGraph_t graph = nullptr;
-        DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
-        const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true);
-        const hipError_t e = hipStreamEndCapture(c->cap, &graph);
+        dis_status r;
+        hipError_t e;
+        {
+            // the capture forks onto the device's pooled sub-batch streams:
+            // no other context's eager work may enter them meanwhile
+            std::lock_guard<std::mutex> lock(pool_mutex(c->device));
+            DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+            r = run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true);
+            e = hipStreamEndCapture(c->cap, &graph);
+        }
         if (r != DIS_OK) {
             if (graph) hipGraphDestroy(graph);
             return r;
         }
         DIS_HIP(e);
         hipError_t e2 = hipErrorUnknown;
-        if (G.exec) {  // same topology (same n and sub-batches): update the parameters in place
+        if (G->exec) {  // same topology (same n and sub-batches): update the parameters in place
             hipGraphExecUpdateResult res;
             hipGraphNode_t bad = nullptr;
-            e2 = hipGraphExecUpdate(G.exec, graph, &bad, &res);
+            e2 = hipGraphExecUpdate(G->exec, graph, &bad, &res);
             if (e2 != hipSuccess) {
                 (void)hipGetLastError();
-                hipGraphExecDestroy(G.exec);
-                G.exec = nullptr;
+                hipGraphExecDestroy(G->exec);
+                G->exec = nullptr;
             }
         }
-        if (!G.exec) e2 = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
+        if (!G->exec) e2 = hipGraphInstantiate(&G->exec, graph, nullptr, nullptr, 0);
         hipGraphDestroy(graph);
         if (e2 != hipSuccess) {
-            G.exec = nullptr;
-            G.n = -1;
+            G->exec = nullptr;
+            G->n = -1;
             DIS_HIP(e2);
         }
-        G.n = n;
-        G.i0 = I0;
-        G.i1 = I1;
-        G.flow = flow;
-        G.stride = stride;
-        G.pair_stride = pair_stride;
-        G.nsub = c->nsub;
-        G.precision = c->precision;
-        G.variant = c->variant;
+        G->n = n;
+        G->i0 = I0;
+        G->i1 = I1;
+        G->flow = flow;
+        G->stride = stride;
+        G->pair_stride = pair_stride;
+        G->nsub = c->nsub;
+        G->precision = c->precision;
+        G->variant = c->variant;
     }
+    G->used = ++c->graph_clock;
     if (c->needs_wait(s)) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     {
         StageRange range("dis: graph launch");
-        DIS_HIP(hipGraphLaunch(G.exec, s));
+        DIS_HIP(hipGraphLaunch(G->exec, s));
     }
+    DIS_HIP(hipEventRecord(G->last, s));
+    G->launched = true;
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
@@ -803,6 +882,7 @@ bool sub_streams(int device, hipStream_t (&out)[dis_ctx::kMaxSub])
 
 // Compat path workspace: one per device for the process, grown on demand.
 struct CompatWs {
+    std::mutex mu;  // one call at a time on this device's workspace and stream
     float *dx = nullptr, *dy = nullptr, *i1 = nullptr;
     float2 *pu = nullptr, *dense = nullptr;
     int* fb = nullptr;
@@ -846,10 +926,11 @@ struct CompatWs {
         return true;
     }
 };
-std::mutex compat_mu;
+std::mutex compat_mu;  // guards the map only: calls on different devices run in parallel
 CompatWs& compat_ws(int device)
 {
-    static std::map<int, CompatWs> ws;  // process lifetime (freed by the driver at exit)
+    static std::map<int, CompatWs> ws;  // process lifetime (freed by the driver at exit); nodes never move
+    std::lock_guard<std::mutex> lock(compat_mu);
     return ws[device];
 }
 
@@ -1065,7 +1146,10 @@ dis_status dis_destroy(dis_ctx* c)
     for (auto& row : c->vrg)
         for (auto& G : row)
             if (G.exec) hipGraphExecDestroy(G.exec);
-    if (c->mg.exec) hipGraphExecDestroy(c->mg.exec);
+    for (auto& G : c->mg) {
+        if (G.exec) hipGraphExecDestroy(G.exec);
+        if (G.last) hipEventDestroy(G.last);
+    }
     if (c->cap) hipStreamDestroy(c->cap);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
@@ -1283,8 +1367,8 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
     // per call would dominate)
     size_t fb_n = dis::kMaxLevels;
     for (int l = g.F; l <= g.C; ++l) fb_n += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8);
-    std::lock_guard<std::mutex> lock(compat_mu);
     CompatWs& w = compat_ws(device);
+    std::lock_guard<std::mutex> lock(w.mu);
     if (!w.reserve(tot, g.u_stride, g.dense_stride, fb_n)) return fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
     hipStream_t s = w.stream;
     const bool fast = g.ps == 8;

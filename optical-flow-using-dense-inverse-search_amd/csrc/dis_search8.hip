@@ -403,7 +403,10 @@ struct BlockLds {
 // dx/dy planes (whatever their padding holds), I1 taps from its padded I1
 // plane clamped to the padded extent -- instead of Sobel of the level image
 // and virtual replicate padding.
-template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false>
+// TSC: the LDS tile row stride as a compile-time constant (0: a.tile_stride at
+// run time). Constant, all 45 taps of an update come from one base address
+// plus ds_read immediate offsets (no per-row address arithmetic).
+template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false, int TSC = 0>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -663,7 +666,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int tx0 = bnd[0] - 10, ty0 = bnd[1] - 10;
     const int tw = bnd[2] + 10 - tx0 + 1, th = bnd[3] + 10 - ty0 + 1;
     const bool use_tile = any_valid && tw <= kTileW<LPP> && th <= kTileH;
-    const int TS = a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
+    const int TS = TSC ? TSC : a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
 
     float u0 = ix, u1 = iy;
     if (use_tile) {
@@ -699,7 +702,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #else
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
 #endif
-                return [base, TS](int k, int c) { return base[k * TS + c]; };
+                return [=](int k, int c) { return base[k * TS + c]; };
             });
         }
     } else if constexpr (kFallback) {
@@ -861,7 +864,7 @@ __global__ void __launch_bounds__(256) k_search_wave(Search8Args a)
 }
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
-template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false, bool kPhys = false>
+template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false, bool kPhys = false, int TSC = 0>
 __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
 k_search8(Search8Args a)
 {
@@ -878,9 +881,9 @@ k_search8(Search8Args a)
     const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
     const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
-    search_block<LPP, kFallback, kPaper, kFma, kPhys>(a, bx, by, bz, S);
+    search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, bx, by, bz, S);
 #else
-    search_block<LPP, kFallback, kPaper, kFma, kPhys>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+    search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
 #endif
 }
 
@@ -968,6 +971,25 @@ bool search8_lpp1_fits(int steps)
     return (15 * steps + 11) * (7 * steps + 10) <= kTileH * kTSMax<1>;
 }
 
+#ifndef DIS_STATIC_TS
+#define DIS_STATIC_TS 1
+#endif
+// k_search8 with the tile stride the host picked (search8_tile_stride) as a
+// template constant: 65, 66, 68 or 72 (every stride tile_layout picks); others
+// at run time
+template <int LPP, bool kFallback, bool kPaper, bool kFma>
+static void launch_ts(const Search8Args& a, dim3 grid, hipStream_t s, Timing t)
+{
+    const dim3 block(kThreads<LPP>);
+    switch (DIS_STATIC_TS ? a.tile_stride : 0) {
+        case 65: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 65>), grid, block, 0, s, a); break;
+        case 66: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 66>), grid, block, 0, s, a); break;
+        case 68: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 68>), grid, block, 0, s, a); break;
+        case 72: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 72>), grid, block, 0, s, a); break;
+        default: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma>), grid, block, 0, s, a); break;
+    }
+}
+
 template <bool kPaper, bool kFma>
 static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid, dim3 fb_grid, hipStream_t s,
                              Timing t)
@@ -981,7 +1003,10 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
         }
     } else if (L == 2) {
         if (split) {
-            DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
+            if constexpr (!kPaper)
+                launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
+            else
+                DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
             hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
@@ -989,7 +1014,10 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     } else if (L == 4) {
         DIS_LAUNCH(t, (k_search8<4, true, kPaper, kFma>), grid, dim3(kThreads<4>), 0, s, a);
     } else {
-        DIS_LAUNCH(t, (k_search8<8, true, kPaper, kFma>), grid, dim3(kThreads<8>), 0, s, a);
+        if constexpr (!kPaper)
+            launch_ts<8, true, kPaper, kFma>(a, grid, s, t);
+        else
+            DIS_LAUNCH(t, (k_search8<8, true, kPaper, kFma>), grid, dim3(kThreads<8>), 0, s, a);
     }
 }
 

@@ -713,6 +713,21 @@ double dis_oracle_var_energy(const float* I0, const float* I1, int stride, int W
     return e;
 }
 
+/* worker threads for the per-level patch loop (1 = the reference's single
+ * thread; OpenMP builds only). Test-side speed knob: results are identical. */
+static int g_threads = 1;
+
+int dis_oracle_set_threads(int n)
+{
+#ifdef _OPENMP
+    g_threads = n < 1 ? 1 : n;
+#else
+    (void)n;
+    g_threads = 1;
+#endif
+    return g_threads;
+}
+
 /* ------------------------------------------------------------------------- */
 /* a15: scale loop (src/optical_flow.cpp:19-91)                                */
 /* ------------------------------------------------------------------------- */
@@ -743,7 +758,6 @@ int dis_oracle_flow_from_pyramids_ex(
     float** flows = (float**)calloc((size_t)nlev, sizeof(float*));
     float** pus = (float**)calloc((size_t)nlev, sizeof(float*));
     size_t dbg_u_off = 0, dbg_d_off = 0;
-    float gdx[1025], gdy[1025], second[1024];
 
     for (int scale = coarsest; scale >= finest; --scale) {       /* :67 */
         level_ctx c;
@@ -768,20 +782,25 @@ int dis_oracle_flow_from_pyramids_ex(
         float* pu = (float*)malloc(sizeof(float) * 2 * (size_t)n);
         float* dense = (scale == finest) ? outflow
                                          : (float*)malloc(sizeof(float) * 2 * (size_t)c.width * c.height);
-        for (int gx = 0; gx < npw; ++gx)
-            for (int gy = 0; gy < nph; ++gy) {
-                const int ip = gx * nph + gy;                    /* src/patch_grid.cpp:39-50 */
-                const float rx = (float)(gx * steps + offw), ry = (float)(gy * steps + offh);
-                float ix = 0.0f, iy = 0.0f;
-                if (scale < coarsest) {                          /* src/patch_grid.cpp:108-119 */
-                    int x = (int)floorf(rx / 2), y = (int)floorf(ry / 2);
-                    int i = y * (c.width / 2) + x;
-                    ix = flows[scale + 1][2 * i] * 2;
-                    iy = flows[scale + 1][2 * i + 1] * 2;
+        /* patches are independent (src/patch_grid.cpp:99-106): the optional
+         * threads (dis_oracle_set_threads) change nothing but the wall time */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(g_threads) if (g_threads > 1)
+#endif
+        for (int ip = 0; ip < n; ++ip) {
+            float gdx[1025], gdy[1025], second[1024];
+            const int gx = ip / nph, gy = ip % nph;          /* ip = gx * nph + gy, src/patch_grid.cpp:39-50 */
+            const float rx = (float)(gx * steps + offw), ry = (float)(gy * steps + offh);
+            float ix = 0.0f, iy = 0.0f;
+            if (scale < coarsest) {                          /* src/patch_grid.cpp:108-119 */
+                int x = (int)floorf(rx / 2), y = (int)floorf(ry / 2);
+                int i = y * (c.width / 2) + x;
+                ix = flows[scale + 1][2 * i] * 2;
+                iy = flows[scale + 1][2 * i + 1] * 2;
                 }
                 patch_search(&c, img_first[scale], img_first_dx[scale], img_first_dy[scale], img_second[scale],
                              rx, ry, ix, iy, gdx, gdy, second, &pu[2 * ip], &pu[2 * ip + 1]);
-            }
+        }
         if (paper_mode)                                          /* SURVEY 8f row 4 */
             densify_paper(&c, npw, nph, steps, offw, offh, pu,
                           img_first[scale] + (size_t)img_padding * c.tmp_w + img_padding,

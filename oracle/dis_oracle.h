@@ -37,6 +37,10 @@ typedef struct {
 
 /* Grid geometry of one level (src/optical_flow.cpp:38, src/patch_grid.cpp:20-23). */
 int dis_oracle_steps(int patch_size, float patch_overlap);
+
+/* Threads for the per-level patch loop (OpenMP builds; default 1). Returns the
+ * count in effect. The patches are independent, so results do not change. */
+int dis_oracle_set_threads(int n);
 void dis_oracle_grid(int width_l, int height_l, int steps,
                      int* npw, int* nph, int* offw, int* offh);
 

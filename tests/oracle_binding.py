@@ -37,6 +37,8 @@ def _load():
     P = ctypes.POINTER
     L.dis_oracle_steps.argtypes = [I, F]
     L.dis_oracle_steps.restype = I
+    L.dis_oracle_set_threads.argtypes = [I]
+    L.dis_oracle_set_threads.restype = I
     L.dis_oracle_grid.argtypes = [I, I, I, P(I), P(I), P(I), P(I)]
     L.dis_oracle_padded_size.argtypes = [I, I, I, P(I), P(I), P(I), P(I)]
     L.dis_oracle_pad_convert.argtypes = [V, Z, I, I, I, V]
@@ -61,6 +63,25 @@ lib = _load()
 
 def _p(a):
     return a.ctypes.data if a is not None else None
+
+
+def set_threads(n):
+    """Threads for the oracle's per-level patch loop (OpenMP); results are
+    identical for every count (the patches are independent). Returns the count."""
+    return lib.dis_oracle_set_threads(int(n))
+
+
+class threads:
+    """Context manager: run the oracle with n patch-loop threads, then back to 1."""
+
+    def __init__(self, n=None):
+        self.n = n if n is not None else min(16, os.cpu_count() or 1)
+
+    def __enter__(self):
+        return set_threads(self.n)
+
+    def __exit__(self, *exc):
+        set_threads(1)
 
 
 def steps(ps, overlap):

@@ -35,6 +35,15 @@ def test_no_oracle_linked_into_product(disflow_mod):
     assert b"dis_oracle" not in data
 
 
+def test_no_hard_profiler_dependency(disflow_mod):
+    # the roctx markers are resolved with dlopen at first use, so the
+    # library loads on a ROCm install without the roctx package
+    import subprocess
+    out = subprocess.run(["readelf", "-d", disflow_mod.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out)
+    assert needed and not [n for n in needed if "roctx" in n or "rocprofiler" in n], needed
+
+
 def test_presets(disflow_mod):
     P = disflow_mod.Preset
     m = disflow_mod.preset_params(P.MEDIUM, 1920, 1080)

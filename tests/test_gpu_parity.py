@@ -245,6 +245,85 @@ def test_graph_replay_matches_eager_and_tracks_its_key(disflow_mod):
     assert np.array_equal(eng.calc_batch(X0, X1).view(np.uint32), out.cpu().numpy().view(np.uint32))
 
 
+def test_graph_cache_ping_pong_without_synchronisation(disflow_mod):
+    # a caller alternating buffer sets on one stream with no
+    # synchronisation. The graph cache keeps an exec per key (LRU of 4) and
+    # never updates an exec while its previous replay may still run: every
+    # output must equal the eager result bit for bit.
+    import torch
+    W, H, B = 640, 480, 2
+    d = disflow_mod
+    p = d.preset_params(d.Preset.MEDIUM, W, H)
+    sets = []
+    for j in range(6):  # 6 keys > the 4 cache slots: evictions under load too
+        pairs = [d.synth_pair(300 + 2 * j + k, W, H) for k in range(B)]
+        sets.append((np.stack([a for a, _ in pairs]), np.stack([b for _, b in pairs])))
+    eager = d.DenseInverseSearch(p, W, H, max_batch=B)
+    eager.set_graphs(False)
+    refs = [eager.calc_batch(X0, X1) for X0, X1 in sets]
+    eng = d.DenseInverseSearch(p, W, H, max_batch=B)
+    s = torch.cuda.Stream()
+    dev = [(torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda()) for X0, X1 in sets]
+    torch.cuda.synchronize()
+    order = [0, 1, 0, 1, 0, 1, 2, 3, 4, 5, 0, 1, 0, 5, 4, 3]
+    outs = []
+    for j in order:
+        out = torch.full((B, H, W, 2), float("nan"), device="cuda")
+        torch.cuda.synchronize()
+        outs.append(out)
+        eng.calc_device(B, dev[j][0].data_ptr(), dev[j][1].data_ptr(), out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    for i, (j, out) in enumerate(zip(order, outs)):
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), refs[j].view(np.uint32)), (i, j)
+
+
+def test_two_threads_two_contexts(disflow_mod):
+    # contexts on one device share the pooled sub-batch streams;
+    # two host threads, each with its own context (graph capture + replay, and
+    # eager calls), must both get their own results bit for bit
+    import threading
+    import torch
+    W, H, B = 640, 480, 4
+    d = disflow_mod
+    p = d.preset_params(d.Preset.MEDIUM, W, H)
+    jobs = []
+    for t in range(2):
+        pairs = [d.synth_pair(500 + 10 * t + k, W, H) for k in range(B)]
+        X0 = np.stack([a for a, _ in pairs])
+        X1 = np.stack([b for _, b in pairs])
+        ref = d.DenseInverseSearch(p, W, H, max_batch=B)
+        ref.set_graphs(False)
+        jobs.append((X0, X1, ref.calc_batch(X0, X1)))
+    errors = []
+
+    def worker(t):
+        try:
+            X0, X1, ref = jobs[t]
+            eng = d.DenseInverseSearch(p, W, H, max_batch=B)
+            s = torch.cuda.Stream()
+            d0, d1 = torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda()
+            out = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
+            for rep in range(12):
+                eng.set_graphs(rep % 3 != 2)  # replays and eager calls interleaved with the other thread's
+                out.fill_(float("nan"))
+                torch.cuda.synchronize()
+                eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+                s.synchronize()
+                if not np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)):
+                    errors.append((t, rep))
+            eng.close()
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "worker thread hung"
+    assert not errors, errors
+
+
 def test_medium_1080p_full_size_bitexact(disflow_mod, oracle):
     # BASELINE config 2 workload at full size against the oracle (a few seconds on CPU)
     W, H = 1920, 1080
