@@ -95,6 +95,21 @@ def cpu_model():
     return None
 
 
+def physical_cores():
+    """Distinct (physical id, core id) pairs in /proc/cpuinfo (SMT siblings
+    counted once); None if the file does not say."""
+    try:
+        cores, phys = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
 def _cpu_worker(args):
     """One host process of the CPU baseline: oracle pairs until the deadline."""
     k0, step, W, H, pfields, deadline = args
@@ -195,13 +210,22 @@ def main():
                "sample": f"{c['pairs']} synthetic {W}x{H} pairs, preset={a.preset}, in {c['cores']} host "
                          f"processes (one pair at a time each, like the reference) for {2 * a.cpu_seconds / 3:.0f} s; "
                          f"C oracle (oracle/dis_oracle.c as {lib}, gcc -O3 -ffp-contract=off)",
-               "host": {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": cpu_model(),
-                        "worker_cap": CPU_WORKER_CAP,
-                        "note": f"workers = min({CPU_WORKER_CAP}, CPUs in this process's affinity mask): "
-                                "the cap is a choice (the GPU box grants one GPU's share of the host, "
-                                "16 CPUs, although nproc shows the whole machine)"},
+               "host": {"nproc": os.cpu_count(), "affinity_cpus": affinity, "physical_cores": physical_cores(),
+                        "cpu_model": cpu_model(), "worker_cap": CPU_WORKER_CAP,
+                        "note": f"measured on {workers} worker processes = min({CPU_WORKER_CAP}, affinity CPUs). "
+                                "The affinity mask shows the whole host, but the GPU pool's operating rules "
+                                f"allot one GPU's share, {CPU_WORKER_CAP} CPUs, to this job and ask worker pools "
+                                "to be sized to it; the whole host (shared with the other GPUs' jobs) is not "
+                                "measured. whole_host_estimate scales the measured per-process rate to the "
+                                "physical cores: an extrapolation, not a measurement"},
                "single_core": {"value": c["single_core"]["value"], "pairs": c["single_core"]["pairs"],
-                               "cores": 1}}
+                               "cores": 1},
+               "per_process": c["value"] / c["cores"]}
+        pc = physical_cores()
+        if pc:
+            cpu["whole_host_estimate"] = {"value": c["value"] / c["cores"] * pc, "cores": pc, "measured": False,
+                                          "basis": f"per-process rate at {c['cores']} workers x {pc} physical cores "
+                                                   "(no SMT gain, no memory-bandwidth loss assumed)"}
     if a.dist_backend != "nccl":  # gloo rehearsal: several ranks may share one GPU
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -305,6 +329,7 @@ def main():
         outs2 = [out, out2]
         for e in engs:
             e.set_concurrency(1)
+        engs[0].pipeline_link(engs[1])  # one batch's head beside the other's body
 
         def pstep(k):
             engs[k % 2].calc_device(B, d0.data_ptr(), d1.data_ptr(), outs2[k % 2].data_ptr(), strs[k % 2].cuda_stream)
@@ -323,6 +348,7 @@ def main():
         if world > 1:
             torch.distributed.all_reduce(el_p, op=torch.distributed.ReduceOp.MAX)
         same = bool(torch.equal(out2.view(torch.int32), out.view(torch.int32)))
+        engs[0].pipeline_link(None)
         engs[1].close()
         del out2
         eng.set_concurrency(a.streams if a.streams else 2)

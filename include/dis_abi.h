@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 4
+#define DIS_ABI_VERSION 5
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -182,6 +182,17 @@ dis_status dis_set_graphs(dis_ctx* ctx, int enable);
 
 typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;
 dis_status dis_set_precision(dis_ctx* ctx, int mode);
+
+/* Two batches in flight (ABI v5; serving, no reference counterpart): link two
+ * contexts on one device whose calls the caller issues alternately on two
+ * streams. Every call of a linked context then starts its front end (pyramid
+ * and coarse levels: latency-bound) only once the peer's latest call has
+ * reached its VALU-bound levels (the search of level F+1), so one batch's head
+ * runs beside the other's body instead of beside the other's head; each
+ * context still orders its own calls on its workspace as usual. Results do not
+ * depend on it. b == NULL unlinks a (and its peer); linking replaces earlier
+ * links of both. */
+dis_status dis_pipeline_link(dis_ctx* a, dis_ctx* b);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
 dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);
 

@@ -176,13 +176,19 @@ struct dis_ctx {
     // that exec's last replay has finished (`last`): the update rewrites the
     // kernel arguments an unstarted node of that replay would still read.
     int graphs = 1;
+    // dis_pipeline_link: the peer context whose calls alternate with ours on
+    // another stream; `body` is recorded by every call of a linked context
+    // just before its level-(F+1) search, and the peer's next call waits for it
+    dis_ctx* peer = nullptr;
+    hipEvent_t body = nullptr;
+    bool body_recorded = false;
     static constexpr int kGraphCache = 4;
     struct MainGraph {
         hipGraphExec_t exec = nullptr;
         hipEvent_t last = nullptr;  // recorded after this exec's latest launch
         bool launched = false;
         unsigned long long used = 0;  // LRU clock
-        int n = -1, nsub = -1, precision = -1, variant = -1;
+        int n = -1, nsub = -1, precision = -1, variant = -1, linked = -1;
         const void *i0 = nullptr, *i1 = nullptr;
         void* flow = nullptr;
         size_t stride = 0, pair_stride = 0;
@@ -408,6 +414,18 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
     return d;
 }
 
+// The first of a call's VALU-bound levels (dis_pipeline_link): the search of
+// level F+1, or F when it is the only level.
+int body_level(const dis::Geometry& g) { return g.C > g.F ? g.F + 1 : g.F; }
+
+// A linked context's call first waits for the peer's latest call to reach its
+// body (on the caller's stream, before anything of this call is enqueued).
+dis_status wait_peer(dis_ctx* c, hipStream_t s)
+{
+    if (c->peer && c->peer->body_recorded) DIS_HIP(hipStreamWaitEvent(s, c->peer->body, 0));
+    return DIS_OK;
+}
+
 // One stage of the path for n pairs already resident in device memory: the
 // front end (pyramid), one level (search, and densify + refinement when on),
 // or the back end (output). run_batches issues the stages stage-major across
@@ -415,7 +433,7 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
 // when the host is slow to enqueue a long stage.
 dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
                      size_t pair_stride, float2* flow, hipStream_t s, int stage, hipEvent_t wait_pyr = nullptr,
-                     hipEvent_t pyr_done = nullptr)
+                     hipEvent_t pyr_done = nullptr, bool capturing = false)
 {
     int* const fb_count = c->fb + (size_t)sub * dis::kMaxLevels;  // this sub-batch's fallback counts
     const dis::Geometry& g = c->g;
@@ -472,6 +490,10 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
+        // dis_pipeline_link: under capture an external event-record node, so
+        // every replay records it (a plain captured record only orders the capture)
+        if (c->peer && sub == 0 && l == body_level(g))
+            DIS_HIP(hipEventRecordWithFlags(c->body, s, capturing ? hipEventRecordExternal : 0));
         dis::SearchArgs a{};
         a.img0 = img0;
         a.img1 = img1;
@@ -706,7 +728,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     if (S <= 1) {
         for (int st : stages) {
             StageRange range(st, 0);
-            dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
+            dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st, nullptr, nullptr, capturing);
             if (r != DIS_OK) return r;
         }
         c->last_batch = n;
@@ -737,7 +759,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
         dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
                                  stride, pair_stride, flow + (size_t)a * fpp, sk, st,
                                  (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
-                                 DIS_STAGGER ? c->staged[k] : nullptr);
+                                 DIS_STAGGER ? c->staged[k] : nullptr, capturing);
         if (r != DIS_OK) return r;
     }
     for (int k = k0; k < S; ++k) {
@@ -758,14 +780,17 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
 dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                              size_t pair_stride, float2* flow, hipStream_t s)
 {
+    if (dis_status w = wait_peer(c, s); w != DIS_OK) return w;
     if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap) {
         std::lock_guard<std::mutex> lock(pool_mutex(c->device));  // eager enqueue onto the pooled streams
-        return run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
+        const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
+        if (r == DIS_OK && c->peer) c->body_recorded = true;
+        return r;
     }
     auto key_is = [&](const dis_ctx::MainGraph& G) {
         return G.exec && G.n == n && G.i0 == I0 && G.i1 == I1 && G.flow == flow && G.stride == stride &&
                G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
-               G.variant == c->variant;
+               G.variant == c->variant && G.linked == (c->peer ? 1 : 0);
     };
     dis_ctx::MainGraph* G = nullptr;
     for (auto& e : c->mg)
@@ -829,6 +854,7 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         G->nsub = c->nsub;
         G->precision = c->precision;
         G->variant = c->variant;
+        G->linked = c->peer ? 1 : 0;
     }
     G->used = ++c->graph_clock;
     if (c->needs_wait(s)) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
@@ -838,6 +864,7 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     }
     DIS_HIP(hipEventRecord(G->last, s));
     G->launched = true;
+    if (c->peer) c->body_recorded = true;  // the graph's event-record node
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
@@ -1085,7 +1112,8 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->body, hipEventDisableTiming) == hipSuccess;
     if (ok) {
         size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
         for (int k = 0; k < dis_ctx::kMaxSub; ++k)
@@ -1118,6 +1146,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
         }
         if (c->fork) hipEventDestroy(c->fork);
         if (c->done) hipEventDestroy(c->done);
+        if (c->body) hipEventDestroy(c->body);
         if (c->cap) hipStreamDestroy(c->cap);
         if (c->own) hipStreamDestroy(c->own);
         delete c;
@@ -1131,6 +1160,11 @@ dis_status dis_destroy(dis_ctx* c)
 {
     if (!c) return DIS_OK;
     hipSetDevice(c->device);
+    if (c->peer) {  // the peer's next call must not wait on our (destroyed) event
+        c->peer->peer = nullptr;
+        c->peer->body_recorded = false;
+        c->peer = nullptr;
+    }
     if (c->own) hipStreamSynchronize(c->own);
     if (c->done_pending) hipEventSynchronize(c->done);  // the last call, on whatever stream it ran
     for (int k = 0; k < dis_ctx::kMaxSub; ++k)  // the streams are shared (process pool): wait for this
@@ -1143,6 +1177,7 @@ dis_status dis_destroy(dis_ctx* c)
     }
     if (c->fork) hipEventDestroy(c->fork);
     if (c->done) hipEventDestroy(c->done);
+    if (c->body) hipEventDestroy(c->body);
     for (auto& row : c->vrg)
         for (auto& G : row)
             if (G.exec) hipGraphExecDestroy(G.exec);
@@ -1214,6 +1249,28 @@ dis_status dis_set_graphs(dis_ctx* c, int enable)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
     c->graphs = enable ? 1 : 0;
+    return DIS_OK;
+}
+
+dis_status dis_pipeline_link(dis_ctx* a, dis_ctx* b)
+{
+    if (!a) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (a == b) return fail(DIS_ERR_INVALID_ARGUMENT, "a context cannot be linked to itself");
+    if (b && b->device != a->device) return fail(DIS_ERR_INVALID_ARGUMENT, "linked contexts must share a device");
+    auto unlink = [](dis_ctx* c) {
+        if (c->peer) {
+            c->peer->peer = nullptr;
+            c->peer->body_recorded = false;
+        }
+        c->peer = nullptr;
+        c->body_recorded = false;
+    };
+    unlink(a);
+    if (b) {
+        unlink(b);
+        a->peer = b;
+        b->peer = a;
+    }
     return DIS_OK;
 }
 

@@ -45,6 +45,9 @@
 #ifndef DIS_S8_EXTRA_ATTR
 #define DIS_S8_EXTRA_ATTR
 #endif
+#ifndef DIS_LOOP_SELECT
+#define DIS_LOOP_SELECT 0
+#endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
 #endif
@@ -352,6 +355,14 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
         const float s2 = ex * ex + ey * ey;
         // sqrtf(s2) > outlierthresh  <=>  s2 > thr_sq (sqrt is correctly rounded
         // and monotone; thr_sq precomputed on the host); NaN -> reset (see oracle)
+#if DIS_LOOP_SELECT
+        // one exit test: the reset as selects, then a single divergent break
+        const bool bad = s2 > a.thr_sq || s2 != s2 || px < a.tmp_lb || py < a.tmp_lb || px > a.tmp_ub_w ||
+                         py > a.tmp_ub_h;
+        u0 = bad ? ix : u0;
+        u1 = bad ? iy : u1;
+        if (bad || counter > a.iters) break;
+#else
         if (s2 > a.thr_sq || s2 != s2 || px < a.tmp_lb || py < a.tmp_lb || px > a.tmp_ub_w ||
             py > a.tmp_ub_h) {
             u0 = ix;
@@ -364,6 +375,7 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 #endif
         }
         if (counter > a.iters) break;
+#endif
     }
     *pu0 = u0;
     *pu1 = u1;

@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "dis_workload_info", "dis_create", "dis_destroy", "dis_calc_u8", "dis_calc_batch_u8",
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
-    "dis_set_concurrency", "dis_set_precision", "dis_set_graphs", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
+    "dis_set_concurrency", "dis_set_precision", "dis_set_graphs", "dis_pipeline_link", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
 )
 
 
@@ -152,6 +152,8 @@ def lib() -> ctypes.CDLL:
         if L.dis_abi_version() >= 4:  # (older builds load for A/B timing only)
             L.dis_set_precision.argtypes = [V, I]
             L.dis_set_graphs.argtypes = [V, I]
+        if L.dis_abi_version() >= 5:
+            L.dis_pipeline_link.argtypes = [V, V]
         L.dis_stage_size.argtypes = [V, I, I, P(Z)]
         L.dis_debug_dump.argtypes = [V, I, I, I, V, Z]
         L.dis_set_kernel_timing.argtypes = [V, I]
@@ -294,6 +296,13 @@ class DenseInverseSearch:
     def set_graphs(self, on: bool = True) -> None:
         """Replay batch calls as captured HIP graphs (default on); results are identical."""
         _check(lib().dis_set_graphs(self._ctx, int(on)))
+
+    def pipeline_link(self, other: "DenseInverseSearch | None") -> None:
+        """Two batches in flight (dis_pipeline_link): with calls issued
+        alternately to this engine and `other` on two streams, each call's
+        front end waits for the peer's latest call to reach its VALU-bound
+        levels. None unlinks. Results are identical."""
+        _check(lib().dis_pipeline_link(self._ctx, other._ctx if other is not None else None))
 
     def set_debug(self, on: bool = True) -> None:
         _check(lib().dis_set_debug(self._ctx, int(on)))

@@ -11,6 +11,7 @@ for `nccl`, gloo on CPU in tests).
 from __future__ import annotations
 
 import hashlib
+import os
 from typing import Callable, Optional, Sequence
 
 import numpy as np
@@ -113,6 +114,21 @@ def run_sharded(I0: np.ndarray, I1: np.ndarray, params, width: int, height: int,
     return out
 
 
+def gather_buffer_bytes(n_total: int, world: int, height: int, width: int) -> int:
+    """Bytes rank 0 allocates to receive the gather: world x (largest shard)
+    flows of height x width x 2 float32 (config 4: 8 x 32 x 16.6 MB = 4.25 GB)."""
+    m = max(shard_bounds(n_total, r, world)[1] - shard_bounds(n_total, r, world)[0] for r in range(world))
+    return world * m * height * width * 2 * 4
+
+
+def check_gather_fits(nbytes: int, free_bytes: int, margin: float = 0.9) -> None:
+    """Raise MemoryError (before any rank blocks in the collective) unless the
+    receive buffer fits in `margin` of the free memory where it is allocated."""
+    if nbytes > margin * free_bytes:
+        raise MemoryError(f"gather needs {nbytes / 1e9:.2f} GB on rank 0, only {free_bytes / 1e9:.2f} GB free "
+                          f"(limit {margin:.0%}): gather checksums instead (gather_checksums)")
+
+
 def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
     """The single collective of the multi-GPU path: gather every
     rank's (n_r, H, W, 2) float32 flows -- device tensors under RCCL (`nccl`),
@@ -134,7 +150,26 @@ def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
         send = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         send[:local.shape[0]] = local
     # rank 0 receives straight into one (world, m, ...) buffer: with equal
-    # shards (the bench case) that buffer IS the result, no second copy
+    # shards (the bench case) that buffer IS the result, no second copy.
+    # Every rank checks rank 0's room first (the verdict is shared through the
+    # group, so no rank is left blocked in the gather when rank 0 cannot
+    # allocate): device memory under RCCL, host memory under gloo.
+    nbytes = world * m * int(np.prod(local.shape[1:])) * local.element_size()
+    ok = torch.ones(1, dtype=torch.int32, device=local.device)
+    err = None
+    if rank == 0:
+        try:
+            if local.is_cuda:
+                free = torch.cuda.mem_get_info(local.device)[0]
+            else:
+                free = os.sysconf("SC_AVPHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+            check_gather_fits(nbytes, free)
+        except MemoryError as e:
+            ok.zero_()
+            err = e
+    dist.broadcast(ok, src=0, group=group)
+    if not int(ok.item()):
+        raise err if err is not None else MemoryError("gather: rank 0 has no room for the receive buffer")
     buf = torch.empty((world,) + tuple(send.shape), dtype=send.dtype, device=send.device) if rank == 0 else None
     recv = list(buf.unbind(0)) if rank == 0 else None
     dist.gather(send.contiguous(), recv, dst=0, group=group)

@@ -277,6 +277,48 @@ def test_graph_cache_ping_pong_without_synchronisation(disflow_mod):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), refs[j].view(np.uint32)), (i, j)
 
 
+def test_linked_contexts_two_batches_in_flight(disflow_mod):
+    # dis_pipeline_link: two contexts, calls alternating on two streams, each
+    # call's front end gated on the peer's latest call reaching its body; every
+    # batch must come out bit for bit (graphs and eager), and unlinking or
+    # destroying one side must leave the other working
+    import torch
+    W, H, B = 640, 480, 4
+    d = disflow_mod
+    p = d.preset_params(d.Preset.MEDIUM, W, H)
+    sets = []
+    for j in range(3):
+        pairs = [d.synth_pair(700 + 5 * j + k, W, H) for k in range(B)]
+        sets.append((np.stack([a for a, _ in pairs]), np.stack([b for _, b in pairs])))
+    ref_eng = d.DenseInverseSearch(p, W, H, max_batch=B)
+    refs = [ref_eng.calc_batch(X0, X1) for X0, X1 in sets]
+    for graphs in (True, False):
+        engs = [d.DenseInverseSearch(p, W, H, max_batch=B) for _ in range(2)]
+        for e in engs:
+            e.set_concurrency(1)
+            e.set_graphs(graphs)
+        engs[0].pipeline_link(engs[1])
+        strs = [torch.cuda.Stream() for _ in range(2)]
+        dev = [(torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda()) for X0, X1 in sets]
+        torch.cuda.synchronize()
+        outs = []
+        for k in range(12):
+            j = k % 3
+            o = torch.full((B, H, W, 2), float("nan"), device="cuda")
+            torch.cuda.synchronize()
+            outs.append((j, o))
+            engs[k % 2].calc_device(B, dev[j][0].data_ptr(), dev[j][1].data_ptr(), o.data_ptr(), strs[k % 2].cuda_stream)
+        torch.cuda.synchronize()
+        for k, (j, o) in enumerate(outs):
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), refs[j].view(np.uint32)), (graphs, k)
+        engs[1].close()  # unlinks: engine 0 keeps working alone
+        got = engs[0].calc_batch(*sets[0])
+        assert np.array_equal(got.view(np.uint32), refs[0].view(np.uint32))
+    with pytest.raises(d.DisError):
+        e = d.DenseInverseSearch(p, W, H)
+        e.pipeline_link(e)
+
+
 def test_two_threads_two_contexts(disflow_mod):
     # contexts on one device share the pooled sub-batch streams;
     # two host threads, each with its own context (graph capture + replay, and

@@ -234,3 +234,51 @@ def test_gloo_gather_checksums_verify_shards(world, n):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok)
+
+
+def test_gather_buffer_size_config4_fits_one_mi355x():
+    # BASELINE config 4: 256 x 1920x1080 pairs over 8 ranks, 32 per rank: rank 0
+    # receives 8 x 32 flows of 16.6 MB = 4.25 GB, far inside 288 GB of HBM
+    nbytes = multi.gather_buffer_bytes(256, 8, 1080, 1920)
+    assert nbytes == 8 * 32 * 1080 * 1920 * 2 * 4
+    assert abs(nbytes / 1e9 - 4.247) < 0.01
+    multi.check_gather_fits(nbytes, 288 * 2**30)
+    with pytest.raises(MemoryError):
+        multi.check_gather_fits(nbytes, 4 * 2**30)
+    # uneven shards: the buffer is world x the largest shard
+    assert multi.gather_buffer_bytes(7, 2, 2, 3) == 2 * 4 * 2 * 3 * 2 * 4
+
+
+def _gather_oom_worker(rank, world, port, out_q):
+    # rank 0 cannot hold the receive buffer: every rank raises MemoryError
+    # promptly instead of blocking in the collective
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=300))
+    multi.check_gather_fits_orig = multi.check_gather_fits
+    multi.check_gather_fits = lambda nbytes, free, margin=0.9: multi.check_gather_fits_orig(nbytes, 1)
+    try:
+        multi.gather_flow_tensor(torch.zeros((2, 4, 5, 2)), 2 * world, rank, world)
+        out_q.put((rank, "no error"))
+    except MemoryError as e:
+        out_q.put((rank, "MemoryError" + (": " + str(e) if rank == 0 else "")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_refuses_when_rank0_has_no_room():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_oom_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=300)
+    assert [g[0] for g in got] == [0, 1]
+    assert all(g[1].startswith("MemoryError") for g in got), got

@@ -379,3 +379,30 @@ def test_rounding_order_spread_within_stated_tolerance(oracle):
         e = tol.epe(tol.with_lib(tol.load_variant(v), oracle.calc_from_params, I0, I1, p), base)
         assert 0 < e.max(), v  # the variants do change the rounding
         assert e.mean() <= stated["mean_epe"] and np.percentile(e, 99.9) <= stated["p999_epe"], v
+
+
+def test_flip_mask_reach():
+    # tests/flipmask.py: a flipped finest-level patch masks its footprint
+    # (+1 level-F pixel for the upsample) at full resolution, nothing else
+    from flipmask import flip_mask, grid, outside_max_epe
+    W, H, C, F, ps, st = 64, 48, 2, 1, 8, 3
+    npw, nph, offw, offh = grid(32, 24, st)
+    u = np.zeros((npw * nph, 2), np.float32)
+    v = u.copy()
+    m, d = flip_mask(u, v, W, H, C, F, ps, st)
+    assert not m.any() and (d == 0).all()
+    gx, gy = 4, 3
+    v[gx * nph + gy] = (0.6, 0.0)
+    m, _ = flip_mask(u, v, W, H, C, F, ps, st)
+    cx, cy = gx * st + offw, gy * st + offh
+    ys, xs = np.nonzero(m)
+    assert (xs.min(), xs.max() + 1) == ((cx - 5) * 2, (cx + 5) * 2)
+    assert (ys.min(), ys.max() + 1) == ((cy - 5) * 2, (cy + 5) * 2)
+    f0 = np.zeros((H, W, 2), np.float32)
+    f1 = f0.copy()
+    f1[ys[0], xs[0]] = (3.0, 4.0)  # inside the site: not counted
+    f1[0, W - 1] = (0.0, 0.25)
+    mx, frac = outside_max_epe(f1, f0, m)
+    assert mx == 0.25 and 0 < frac < 1
+    v[0] = (np.nan, 0.0)  # NaN counts as a flip
+    assert flip_mask(u, v, W, H, C, F, ps, st)[0][0, 0]

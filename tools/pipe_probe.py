@@ -44,6 +44,10 @@ for e in (ea, eb):
     e.set_concurrency(1)
 sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
 print("two engines on two streams, 1 sub-batch each:", round(run([ea, eb], [sa, sb], K)))
+ea.pipeline_link(eb)
+print("  linked (dis_pipeline_link):", round(run([ea, eb], [sa, sb], K)))
+print("  linked, 40 batches:", round(run([ea, eb], [sa, sb], 40)))
+ea.pipeline_link(None)
 for e in (ea, eb):
     e.set_concurrency(2)
 print("two engines on two streams, 2 sub-batches each:", round(run([ea, eb], [sa, sb], K)))
