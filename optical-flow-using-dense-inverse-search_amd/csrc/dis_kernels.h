@@ -149,6 +149,10 @@ struct OutputArgs {
 };
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t = {});
+// the same planes by two streaming kernels (dis_pyramid.hip): levels 1-2 from
+// global memory, then levels 3..a.levels; needs a.levels >= 2
+bool pyramid2_fits(const PyramidArgs& a);
+hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timing t = {});
 bool output_fits(const OutputArgs& a);
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_level0(const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,

@@ -126,6 +126,9 @@ static int search8_lanes(int variant, long long patches, int steps)
     return big;
 }
 
+#ifndef DIS_PYR2
+#define DIS_PYR2 1  // the two-kernel streaming pyramid (dis_pyramid.hip) where it fits
+#endif
 #ifndef DIS_QUAD_LAYOUT
 #define DIS_QUAD_LAYOUT 1  // LPP-2 4 x 4-patch half-waves where they spread the LDS banks better
 #endif
@@ -476,7 +479,10 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
                 pa.off[l] = g.lv[l].plane_off;
                 pa.w[l] = g.lv[l].W;
             }
-            DIS_HIP(dis::launch_pyramid(pa, n, s, timing(c, 0)));
+            if (DIS_PYR2 && dis::pyramid2_fits(pa))
+                DIS_HIP(dis::launch_pyramid2(pa, n, s, timing(c, 0)));
+            else
+                DIS_HIP(dis::launch_pyramid(pa, n, s, timing(c, 0)));
             for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
             if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
@@ -490,10 +496,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
-        // dis_pipeline_link: under capture an external event-record node, so
-        // every replay records it (a plain captured record only orders the capture)
-        if (c->peer && sub == 0 && l == body_level(g))
-            DIS_HIP(hipEventRecordWithFlags(c->body, s, capturing ? hipEventRecordExternal : 0));
+        // dis_pipeline_link (linked calls run eagerly: see run_batches_graph)
+        if (c->peer && sub == 0 && l == body_level(g) && !capturing) DIS_HIP(hipEventRecord(c->body, s));
         dis::SearchArgs a{};
         a.img0 = img0;
         a.img1 = img1;
@@ -781,7 +785,11 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
                              size_t pair_stride, float2* flow, hipStream_t s)
 {
     if (dis_status w = wait_peer(c, s); w != DIS_OK) return w;
-    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap) {
+    // eager: graphs off, kernel timing, debug dumps, refinement (its own
+    // per-level graphs), and linked contexts (the body event is recorded in
+    // the middle of the call; HIP rejects an external event-record node
+    // under stream capture)
+    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap || c->peer) {
         std::lock_guard<std::mutex> lock(pool_mutex(c->device));  // eager enqueue onto the pooled streams
         const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
         if (r == DIS_OK && c->peer) c->body_recorded = true;
