@@ -175,9 +175,12 @@ dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
  * once per (n, frame/flow pointers and strides, concurrency, precision,
  * variant) and replayed as one graph -- the fork into the sub-batch streams,
  * every level's launches and the join -- instead of ~25 eager launches; a
- * changed key re-captures (the executable graph is updated in place). Kernel
- * timing, debug dumps and variational refinement run eagerly. Results do not
- * depend on this setting. */
+ * changed key re-captures (an LRU of four executable graphs per context; an
+ * exec is updated only after its previous replay has finished). Kernel timing,
+ * debug dumps, variational refinement and linked contexts run eagerly. The
+ * capture is thread-local: if another thread synchronises the device or uses
+ * the legacy default stream meanwhile, HIP invalidates it and that call runs
+ * eagerly instead. Results do not depend on this setting. */
 dis_status dis_set_graphs(dis_ctx* ctx, int enable);
 
 typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;

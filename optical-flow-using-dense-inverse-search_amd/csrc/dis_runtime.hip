@@ -821,37 +821,41 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         StageRange range("dis: graph capture");
         hipGraph_t graph = nullptr;
         dis_status r;
-        hipError_t e;
+        hipError_t e, e0;
         {
             // the capture forks onto the device's pooled sub-batch streams:
             // no other context's eager work may enter them meanwhile
             std::lock_guard<std::mutex> lock(pool_mutex(c->device));
-            DIS_HIP(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
-            r = run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true);
-            e = hipStreamEndCapture(c->cap, &graph);
+            e0 = hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal);
+            r = e0 == hipSuccess ? run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true) : DIS_OK;
+            e = e0 == hipSuccess ? hipStreamEndCapture(c->cap, &graph) : e0;
         }
-        if (r != DIS_OK) {
-            if (graph) hipGraphDestroy(graph);
-            return r;
-        }
-        DIS_HIP(e);
         hipError_t e2 = hipErrorUnknown;
-        if (G->exec) {  // same topology (same n and sub-batches): update the parameters in place
-            hipGraphExecUpdateResult res;
-            hipGraphNode_t bad = nullptr;
-            e2 = hipGraphExecUpdate(G->exec, graph, &bad, &res);
-            if (e2 != hipSuccess) {
-                (void)hipGetLastError();
-                hipGraphExecDestroy(G->exec);
-                G->exec = nullptr;
+        if (r == DIS_OK && e == hipSuccess) {
+            if (G->exec) {  // same topology (same n and sub-batches): update the parameters in place
+                hipGraphExecUpdateResult res;
+                hipGraphNode_t bad = nullptr;
+                e2 = hipGraphExecUpdate(G->exec, graph, &bad, &res);
+                if (e2 != hipSuccess) {
+                    (void)hipGetLastError();
+                    hipGraphExecDestroy(G->exec);
+                    G->exec = nullptr;
+                }
             }
+            if (!G->exec) e2 = hipGraphInstantiate(&G->exec, graph, nullptr, nullptr, 0);
         }
-        if (!G->exec) e2 = hipGraphInstantiate(&G->exec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
+        if (graph) hipGraphDestroy(graph);
         if (e2 != hipSuccess) {
+            // The capture was invalidated (e.g. another thread synchronised the
+            // device or used the legacy default stream meanwhile) or failed to
+            // instantiate: this call runs eagerly -- same results -- and the
+            // next call with this key tries to capture again.
+            (void)hipGetLastError();
+            if (G->exec) hipGraphExecDestroy(G->exec);
             G->exec = nullptr;
             G->n = -1;
-            DIS_HIP(e2);
+            std::lock_guard<std::mutex> lock(pool_mutex(c->device));
+            return run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
         }
         G->n = n;
         G->i0 = I0;

@@ -342,17 +342,22 @@ def test_two_threads_two_contexts(disflow_mod):
         try:
             X0, X1, ref = jobs[t]
             eng = d.DenseInverseSearch(p, W, H, max_batch=B)
+            # every torch operation of this thread on its own stream: no
+            # device-wide synchronisation while the other thread may be
+            # capturing (HIP fails an in-progress capture then; the library
+            # would fall back to an eager call, the caller's op would fail)
             s = torch.cuda.Stream()
-            d0, d1 = torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda()
-            out = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
-            for rep in range(12):
-                eng.set_graphs(rep % 3 != 2)  # replays and eager calls interleaved with the other thread's
-                out.fill_(float("nan"))
-                torch.cuda.synchronize()
-                eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
-                s.synchronize()
-                if not np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)):
-                    errors.append((t, rep))
+            with torch.cuda.stream(s):
+                d0, d1 = torch.from_numpy(X0).cuda(), torch.from_numpy(X1).cuda()
+                out = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
+                for rep in range(12):
+                    eng.set_graphs(rep % 3 != 2)  # replays and eager calls interleaved with the other thread's
+                    out.fill_(float("nan"))
+                    eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
+                    host = out.to("cpu", non_blocking=False)
+                    s.synchronize()
+                    if not np.array_equal(host.numpy().view(np.uint32), ref.view(np.uint32)):
+                        errors.append((t, rep))
             eng.close()
         except Exception as e:  # pragma: no cover - surfaced below
             errors.append((t, repr(e)))

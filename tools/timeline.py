@@ -12,7 +12,7 @@ def main():
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 24
     rows = [r for r in csv.DictReader(open(path)) if "copyBuffer" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    pyr = [i for i, r in enumerate(rows) if "pyramid" in r["Kernel_Name"]]
+    pyr = [i for i, r in enumerate(rows) if "pyramid" in r["Kernel_Name"] or "k_pyr12" in r["Kernel_Name"]]
     i0 = pyr[min(k, len(pyr) - 1)]
     t0 = int(rows[i0]["Start_Timestamp"])
     for r in rows[i0:i0 + n]:
