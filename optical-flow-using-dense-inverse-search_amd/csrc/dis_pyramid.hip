@@ -2,14 +2,13 @@
 // frames, no workgroup barriers on the bandwidth-heavy part):
 //
 //   k_pyr12: u8 frame -> (virtual) pad -> level-0 Sobel magnitude -> levels 1
-//            and 2, straight from global memory. One lane = one level-2 pixel
-//            = a 4x4 block of level-0 magnitudes from its 6x6 u8 window
-//            (src/main.cpp:16-30, 139-160); a wave covers 64 consecutive
-//            level-2 pixels of one row, so its u8 row loads are one dword per
-//            lane (256 contiguous bytes) and the window's halo columns come
-//            from the neighbour lanes (DPP wave shifts); its level-1 stores
-//            are 8 contiguous bytes per lane (512 B per row), level 2 one
-//            float per lane.
+//            and 2, straight from global memory. One lane = four consecutive
+//            level-2 pixels = 4x4 blocks of level-0 magnitudes from a 6x18 u8
+//            window (src/main.cpp:16-30, 139-160); a wave covers 256
+//            consecutive level-2 pixels of one row, so its u8 row loads are
+//            one 16-byte load per lane (1 KB contiguous) and the window's halo
+//            columns come from the neighbour lanes (DPP wave shifts); its
+//            level-1 and level-2 stores are 16-byte stores.
 //   k_pyr_tail: levels 3..L (L <= 6) from level 2, one wave per 2^(L-2)
 //            square of level-2 pixels, intermediate levels in LDS.
 //
@@ -59,92 +58,187 @@ __device__ __forceinline__ int src_col(const PyramidArgs& a, int x)
 
 }  // namespace
 
-// grid: (ceil(W2 / 64), H2, 2 * batch) waves of 64 lanes; z = 2 * pair + frame
-__global__ void __launch_bounds__(64) k_pyr12(PyramidArgs a)
+// Sobel magnitudes (x 8) of the 4x4 level-0 block whose 6x6 u8 window rows
+// are the bytes (byte 3 of p, bytes 0..3 of m, byte 0 of n) of dwords p, m, n,
+// then its level-1 2x2 block and level-2 pixel. Integer Sobel in packed 16-bit
+// lanes (exact: |values| <= 1020): per window row and column c,
+// X = (R, T) = (v[c+2] - v[c], 2 v[c+1] + v[c] + v[c+2]); per pixel
+// q = (k1, k2) = (2 R1 + R0 + R2, T2 - T0) = X1 (2,0) + X0 (1,-1) + X2 and
+// N = k1^2 + k2^2 = dot2(q, q), gx^2 + gy^2 = N / 64 exactly.
+struct Block4 {
+    float m[4][4];   // 8 x the level-0 magnitudes
+    float l1[2][2];  // level 1
+    float l2;        // level 2
+};
+
+__device__ __forceinline__ void block4(const unsigned (&p)[6], const unsigned (&m)[6], const unsigned (&n)[6],
+                                       Block4& o)
+{
+    // rows streamed: X of three window rows live at a time, the magnitudes of
+    // one level-1 row (two level-0 rows) at a time (bounded registers)
+    const short2p cm11 = {-1, 1}, c02 = {0, 2}, c20 = {2, 0}, c1m1 = {1, -1};
+    short2p X[3][4];
+    auto xrow = [&](int r, short2p (&x)[4]) {
+        const short2p B[6] = {bytes2<3, 3>(p[r], m[r]), bytes2<4, 4>(p[r], m[r]), bytes2<5, 5>(p[r], m[r]),
+                              bytes2<6, 6>(p[r], m[r]), bytes2<7, 7>(p[r], m[r]), bytes2<4, 4>(m[r], n[r])};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[c] = B[c] * cm11 + (B[c + 1] * c02 + B[c + 2]);
+    };
+    xrow(0, X[0]);
+    xrow(1, X[1]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        xrow(r + 2, X[(r + 2) % 3]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const short2p q = X[(r + 1) % 3][c] * c20 + (X[r % 3][c] * c1m1 + X[(r + 2) % 3][c]);
+            int nn;
+            __asm__("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(nn) : "v"(q));
+            o.m[r][c] = sqrt_cr((float)nn);
+        }
+        if (r & 1) {
+            // level 1: ((m00 + m01) + m10) + m11 of the 8x-scaled magnitudes x
+            // 2^-5 (= the reference's 2x2 mean of the unscaled ones: powers of
+            // two commute with the roundings)
+            const int i = r >> 1;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                float s = o.m[2 * i][2 * j] + o.m[2 * i][2 * j + 1];
+                s = s + o.m[2 * i + 1][2 * j];
+                s = s + o.m[2 * i + 1][2 * j + 1];
+                o.l1[i][j] = s * 0.03125f;
+            }
+        }
+    }
+    // level 2: the 2x2 mean of level 1
+    float s = o.l1[0][0] + o.l1[0][1];
+    s = s + o.l1[1][0];
+    s = s + o.l1[1][1];
+    o.l2 = s * 0.25f;
+}
+
+// grid: (ceil(W2 / 256), H2, 2 * batch) waves; z = 2 * pair + frame. Lane =
+// 4 consecutive level-2 pixels of row y2 = level-0 columns x0 .. x0 + 15
+// (x0 = 16 g), window columns x0 - 1 .. x0 + 16, rows 4 y2 - 1 .. 4 y2 + 4.
+#ifndef DIS_PYR12_WAVES
+#define DIS_PYR12_WAVES 5  // min waves per SIMD: 91 VGPRs, no spills (6: 80 + 48 B scratch)
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12(PyramidArgs a)
 {
     const int lane = threadIdx.x;
     const int W2 = a.w[2];
     const int y2 = blockIdx.y;
-    const int x2 = blockIdx.x * 64 + lane;
+    const int g = blockIdx.x * 64 + lane;  // lane's group of 4 level-2 pixels
     const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
     if (blockIdx.x == 0 && y2 == 0 && blockIdx.z == 0 && lane < a.nzero) a.zero[lane] = 0;
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-    const bool inx = x2 < W2;
-    const int xc = inx ? x2 : W2 - 1;  // idle lanes mirror the last column (their loads stay in bounds)
-    // window: level-0 columns x0 - 1 .. x0 + 4, rows 4 y2 - 1 .. 4 y2 + 4
-    const int x0 = 4 * xc;
-    // body dword: the window's columns x0 .. x0 + 3 are source columns
-    // x0 - pl .. x0 - pl + 3 (no clamping; dword_ok: aligned); the halo columns
-    // are then the neighbour lanes' body bytes (DPP wave shifts), except at the
-    // wave's ends, the plane's edges (reflect-101) and the padding (clamping),
-    // where the lane loads its halo byte itself
-    const bool body = a.dword_ok && x0 >= a.pl && x0 + 3 - a.pl <= a.W - 1;
-    const bool nb_l = body && lane > 0 && x0 - 4 >= a.pl;
-    const bool nb_r = body && lane < 63 && x0 + 7 - a.pl <= a.W - 1 && x2 + 1 < W2;
-    short2p X[6][4];
+    const int ng = (W2 + 3) >> 2;                 // groups per row
+    const int gc = g < ng ? g : ng - 1;           // idle lanes mirror the last group (loads stay in bounds)
+    const int x0 = 16 * gc;
+    // body: the window's columns x0 .. x0 + 15 are source columns x0 - pl ..
+    // (no clamping; qword_ok: 16-byte aligned rows) -- one 16-byte load per
+    // row; the halo columns are then the neighbour lanes' body bytes (DPP wave
+    // shifts), except at the wave's ends, the plane's edges (reflect-101) and
+    // the padding (clamping), where the lane loads its halo byte itself
+    const bool body = a.qword_ok && x0 >= a.pl && x0 + 15 - a.pl <= a.W - 1;
+    const bool nb_l = body && lane > 0 && x0 - 16 >= a.pl;
+    const bool nb_r = body && lane < 63 && x0 + 31 - a.pl <= a.W - 1 && g + 1 < ng;
+    unsigned d[4][6], wl[6], wr[6];
+    const uint8_t* rows[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) rows[r] = in + (size_t)src_row(a, 4 * y2 - 1 + r) * a.stride;
+    // every row's load in flight before any is consumed (no branch between
+    // them): the 16-byte body loads of all lanes (lanes without a body read a
+    // harmless in-bounds 16 bytes, W >= 16), then the byte gathers of the
+    // lanes that need them (exec-masked, all issued before the wait)
+    if (a.qword_ok && a.W >= 16) {
+        const int xb = body ? x0 - a.pl : 0;
+        uint4 v[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v[r] = *reinterpret_cast<const uint4*>(rows[r] + xb);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            d[0][r] = v[r].x;
+            d[1][r] = v[r].y;
+            d[2][r] = v[r].z;
+            d[3][r] = v[r].w;
+        }
+    }
+    if (!body) {  // padding columns, unaligned frames: bytes
+        uint8_t bb[6][16];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bb[r][k] = rows[r][src_col(a, x0 + k)];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                d[k][r] = (unsigned)bb[r][4 * k] | ((unsigned)bb[r][4 * k + 1] << 8) |
+                          ((unsigned)bb[r][4 * k + 2] << 16) | ((unsigned)bb[r][4 * k + 3] << 24);
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const uint8_t* row = in + (size_t)src_row(a, 4 * y2 - 1 + r) * a.stride;
-        unsigned wm;
-        if (body) {
-            wm = *reinterpret_cast<const unsigned*>(row + x0 - a.pl);
-        } else {  // padding columns, unaligned frames: bytes
-            wm = (unsigned)row[src_col(a, x0)] | ((unsigned)row[src_col(a, x0 + 1)] << 8) |
-                 ((unsigned)row[src_col(a, x0 + 2)] << 16) | ((unsigned)row[src_col(a, x0 + 3)] << 24);
-        }
-        unsigned wl = wave_shr1(wm, 0u), wr = wave_shl1(wm, 0u);
-        if (!nb_l) wl = (unsigned)row[src_col(a, x0 - 1)] << 24;
-        if (!nb_r) wr = (unsigned)row[src_col(a, x0 + 4)];
-        // window columns 0..5 = byte 3 of wl, bytes 0..3 of wm, byte 0 of wr,
-        // each broadcast to both 16-bit lanes
-        const short2p B[6] = {bytes2<3, 3>(wl, wm), bytes2<4, 4>(wl, wm), bytes2<5, 5>(wl, wm),
-                              bytes2<6, 6>(wl, wm), bytes2<7, 7>(wl, wm), bytes2<4, 4>(wm, wr)};
-        // (R, T) = (v[c+2] - v[c], 2 v[c+1] + v[c] + v[c+2]) per column c
-        const short2p cm11 = {-1, 1}, c02 = {0, 2};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) X[r][c] = B[c] * cm11 + (B[c + 1] * c02 + B[c + 2]);
+        wl[r] = wave_shr1(d[3][r], 0u);
+        wr[r] = wave_shl1(d[0][r], 0u);
     }
-    // level-0 magnitudes x 8: q = (k1, k2) = (2 R1 + R0 + R2, T2 - T0), N = k1^2 + k2^2
-    float m[4][4];
-    const short2p c20 = {2, 0}, c1m1 = {1, -1};
+    if (!nb_l || !nb_r) {  // the wave's end lanes, the plane's edges, the padding
+        const int cl = src_col(a, x0 - 1), cr = src_col(a, x0 + 16);
+        uint8_t hl[6], hr[6];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const short2p q = X[r + 1][c] * c20 + (X[r][c] * c1m1 + X[r + 2][c]);
-            int n;
-            __asm__("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(n) : "v"(q));
-            m[r][c] = sqrt_cr((float)n);
+        for (int r = 0; r < 6; ++r) {
+            hl[r] = rows[r][cl];
+            hr[r] = rows[r][cr];
         }
-    if (!inx) return;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            if (!nb_l) wl[r] = (unsigned)hl[r] << 24;
+            if (!nb_r) wr[r] = (unsigned)hr[r];
+        }
+    }
+    if (g >= ng) return;
     float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
-    if (a.write_l0) {
+    const int np = min(4, W2 - 4 * g);  // level-2 pixels of this lane (the row's last group may be short)
+    float l1row[2][8], l2v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float4 v = make_float4(m[r][0] * 0.125f, m[r][1] * 0.125f, m[r][2] * 0.125f, m[r][3] * 0.125f);
-            *reinterpret_cast<float4*>(planes + (size_t)(4 * y2 + r) * a.Wp + x0) = v;
+    for (int q = 0; q < 4; ++q) {
+        Block4 o;
+        block4(q == 0 ? wl : d[q - 1], d[q], q == 3 ? wr : d[q + 1], o);
+        if (a.write_l0 && q < np) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                *reinterpret_cast<float4*>(planes + (size_t)(4 * y2 + r) * a.Wp + x0 + 4 * q) =
+                    make_float4(o.m[r][0] * 0.125f, o.m[r][1] * 0.125f, o.m[r][2] * 0.125f, o.m[r][3] * 0.125f);
         }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            l1row[i][2 * q] = o.l1[i][0];
+            l1row[i][2 * q + 1] = o.l1[i][1];
+        }
+        l2v[q] = o.l2;
     }
-    // level 1: ((m00 + m01) + m10) + m11 of the 8x-scaled magnitudes x 2^-5
-    // (= the reference's 2x2 mean of the unscaled ones: powers of two commute
-    // with the roundings); level 2: the 2x2 mean of level 1
-    float l1[2][2];
+    float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 8 * g;
+    float* p2 = planes + a.off[2] + (size_t)y2 * W2 + 4 * g;
+    if (np == 4) {  // 16-byte stores (level-1 rows and the level-2 plane are 16-byte aligned: W % 16 == 0 here)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            float s = m[2 * i][2 * j] + m[2 * i][2 * j + 1];
-            s = s + m[2 * i + 1][2 * j];
-            s = s + m[2 * i + 1][2 * j + 1];
-            l1[i][j] = s * 0.03125f;
+        for (int i = 0; i < 2; ++i) {
+            *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1]) =
+                make_float4(l1row[i][0], l1row[i][1], l1row[i][2], l1row[i][3]);
+            *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1] + 4) =
+                make_float4(l1row[i][4], l1row[i][5], l1row[i][6], l1row[i][7]);
         }
-    float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 2 * x2;
-    *reinterpret_cast<float2*>(p1) = make_float2(l1[0][0], l1[0][1]);
-    *reinterpret_cast<float2*>(p1 + a.w[1]) = make_float2(l1[1][0], l1[1][1]);
-    float s = l1[0][0] + l1[0][1];
-    s = s + l1[1][0];
-    s = s + l1[1][1];
-    planes[a.off[2] + (size_t)y2 * W2 + x2] = s * 0.25f;
+        *reinterpret_cast<float4*>(p2) = make_float4(l2v[0], l2v[1], l2v[2], l2v[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q < np) {
+                p1[2 * q] = l1row[0][2 * q];
+                p1[2 * q + 1] = l1row[0][2 * q + 1];
+                p1[a.w[1] + 2 * q] = l1row[1][2 * q];
+                p1[a.w[1] + 2 * q + 1] = l1row[1][2 * q + 1];
+                p2[q] = l2v[q];
+            }
+    }
 }
 
 // grid: (W2 / T2, H2 / T2, 2 * batch), T2 = 2^(L-2) level-2 pixels per tile
@@ -199,7 +293,7 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     if (!pyramid2_fits(a) || a.nzero > 64) return hipErrorInvalidValue;
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
-    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 63) / 64, H2, 2 * batch), dim3(64), 0, s, a);
+    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, H2, 2 * batch), dim3(64), 0, s, a);
     if (a.levels >= 3) {
         const int T2 = 1 << (a.levels - 2);
         const dim3 grid(W2 / T2, H2 / T2, 2 * batch);

@@ -46,7 +46,7 @@
 #define DIS_S8_EXTRA_ATTR
 #endif
 #ifndef DIS_LOOP_SELECT
-#define DIS_LOOP_SELECT 0
+#define DIS_LOOP_SELECT 1
 #endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
@@ -381,35 +381,8 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
     *pu1 = u1;
 }
 
-// A block whose start positions are too spread for the LDS tile, searched in
-// place by its own workgroup with the taps read through L1/L2 (identical
-// results). Not inlined: the rare path gets its own register allocation, so
-// the tile path keeps 4 waves per SIMD (this callee may spill) and no separate
-// fallback launch has to wait for slots behind a co-running search.
-template <int LPP, bool kPaper, bool kFma, bool kPhys>
-__device__ __attribute__((noinline)) void spread_block_search(const Search8Args& a, const LU2& lu,
-                                                              const float (&gx)[8 * kNCol<LPP>],
-                                                              const float (&gy)[8 * kNCol<LPP>], float rx,
-                                                              float ry, float ix, float iy, float bt0, float bt1,
-                                                              int q, int pair, float* pu0, float* pu1)
-{
-    const int W = a.W, H = a.H;
-    const int pad = kPhys ? a.pad : 0, ld = W + 2 * pad, lo = -pad;
-    const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off + (kPhys ? pad * ld + pad : 0);
-    const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
-    iterate<LPP, true, kPaper, kFma>(a, lu, gx, gy, rx, ry, ix, iy, bt0, bt1, pu0, pu1, [&](const Warp& w) {
-        const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
-        return [=](int k, int c) {
-            return I1[(ptrdiff_t)clampi(y0 + k, lo, H - 1 + pad) * ld + clampi(x0 + c, lo, W - 1 + pad)];
-        };
-    });
-}
-
 }  // namespace
 
-#ifndef DIS_FB_CALL
-#define DIS_FB_CALL 0  // spread blocks: in-kernel non-inlined search instead of a k_search8_fb launch
-#endif
 #ifndef DIS_XCD_REMAP
 #define DIS_XCD_REMAP 1
 #endif
@@ -754,10 +727,6 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 };
             });
         }
-    } else if (DIS_FB_CALL && any_valid) {
-        // too spread for the tile: search it here through L1/L2 (rare)
-        if (valid) spread_block_search<LPP, kPaper, kFma, kPhys>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, q, pair,
-                                                                 &u0, &u1);
     } else if (any_valid) {
         // too spread for the tile: k_search8_fb redoes this block
         if (tid == 0) {
@@ -1040,8 +1009,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     if (L == 1) {
         if (split) {
             DIS_LAUNCH(t, (k_search8<1, false, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
-            if (!DIS_FB_CALL)
-                hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<1, true, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
         }
@@ -1051,8 +1019,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
                 launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             else
                 DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
-            if (!DIS_FB_CALL)
-                hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
         }
@@ -1073,8 +1040,7 @@ static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 gr
     if (L == 2) {
         if (split) {
             hipLaunchKernelGGL((k_search8<2, false, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
-            if (!DIS_FB_CALL)
-                hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             hipLaunchKernelGGL((k_search8<2, true, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
         }
@@ -1099,10 +1065,11 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     if (L != 1 && (7 * a.steps + 11) * (7 * a.steps + 10) > kTileH * kTSMax<2>) return hipErrorInvalidValue;
     const int bx = L == 1 ? kBX<1> : kBX<2>;
     dim3 grid((a.npw + bx - 1) / bx, (a.nph + kBY - 1) / kBY, batch);
-    // split: the tile-only kernel (4 waves per SIMD at LPP 2) and, unless the
-    // tile kernel searches spread blocks itself (DIS_FB_CALL), a k_search8_fb
-    // launch over the blocks it listed
-    const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && (DIS_FB_CALL || (a.fb_count && a.fb_list));
+    // split: the tile-only kernel (4 waves per SIMD at LPP 2) and a
+    // k_search8_fb launch over the blocks it listed. (Searching those blocks
+    // in place through a non-inlined call instead made every wave of the tile
+    // kernel carry a scratch frame: finest launch 940 -> 1346 us; r03.)
+    const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
     if (a.gdx_plane) {  // physical planes (compat): exact, non-paper, LPP 2 or 8
