@@ -120,6 +120,9 @@ __device__ __forceinline__ void block4(const unsigned (&p)[6], const unsigned (&
 // grid: (ceil(W2 / 256), H2, 2 * batch) waves; z = 2 * pair + frame. Lane =
 // 4 consecutive level-2 pixels of row y2 = level-0 columns x0 .. x0 + 15
 // (x0 = 16 g), window columns x0 - 1 .. x0 + 16, rows 4 y2 - 1 .. 4 y2 + 4.
+#ifndef DIS_PYR12_XCD
+#define DIS_PYR12_XCD 0  // r03 A/B: HBM bytes 397 -> 300 MB per 32 pairs, but 98 -> 115 us
+#endif
 #ifndef DIS_PYR12_WAVES
 #define DIS_PYR12_WAVES 5  // min waves per SIMD: 91 VGPRs, no spills (6: 80 + 48 B scratch)
 #endif
@@ -127,10 +130,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
 {
     const int lane = threadIdx.x;
     const int W2 = a.w[2];
-    const int y2 = blockIdx.y;
-    const int g = blockIdx.x * 64 + lane;  // lane's group of 4 level-2 pixels
-    const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
-    if (blockIdx.x == 0 && y2 == 0 && blockIdx.z == 0 && lane < a.nzero) a.zero[lane] = 0;
+#if DIS_PYR12_XCD
+    // XCD-aware wave order (off: measured slower, see the macro): the
+    // dispatcher deals linear workgroup ids round-robin to the 8 XCDs; remap
+    // so each XCD walks a contiguous run of rows and the two level-0 halo rows
+    // a wave shares with the next row's wave are read from HBM once
+    const int nbx = gridDim.x, nby = gridDim.y, nb = nbx * nby * gridDim.z;
+    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    const int per = nb / 8;
+    const int t = lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
+    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
+    const int y2 = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
+#else
+    const int bx = blockIdx.x, y2 = blockIdx.y, bz = blockIdx.z;
+#endif
+    const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
+    const int pair = bz >> 1, frame = bz & 1;
+    if (bx == 0 && y2 == 0 && bz == 0 && lane < a.nzero) a.zero[lane] = 0;
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
     const int ng = (W2 + 3) >> 2;                 // groups per row
     const int gc = g < ng ? g : ng - 1;           // idle lanes mirror the last group (loads stay in bounds)
