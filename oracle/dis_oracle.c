@@ -23,6 +23,17 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* worker threads (1 = the reference's single thread; OpenMP builds only) for
+ * the per-level patch loop and the per-pixel stages (rows split among threads;
+ * densify split into row bands that each keep the patch-id accumulation
+ * order). A test-side speed knob: results are identical for every count. */
+static int g_threads = 1;
+#ifdef _OPENMP
+#define DIS_OMP_ROWS _Pragma("omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)")
+#else
+#define DIS_OMP_ROWS
+#endif
+
 /* ------------------------------------------------------------------------- */
 /* Eigen-order helpers                                                        */
 /* ------------------------------------------------------------------------- */
@@ -138,6 +149,7 @@ void dis_oracle_pad_convert(const uint8_t* in, size_t stride, int W, int H,
     int Wp, Hp, pl, pt;
     dis_oracle_padded_size(W, H, coarsest, &Wp, &Hp, &pl, &pt);
     /* copyMakeBorder BORDER_REPLICATE (:152-153), convertTo(CV_32F) (:159) */
+    DIS_OMP_ROWS
     for (int y = 0; y < Hp; ++y) {
         const uint8_t* row = in + (size_t)clampi(y - pt, 0, H - 1) * stride;
         for (int x = 0; x < Wp; ++x)
@@ -169,6 +181,7 @@ void dis_oracle_sobel(const float* src, int W, int H, float* dx, float* dy)
 {
     float* R = (float*)malloc(sizeof(float) * (size_t)W * H);
     float* S = (float*)malloc(sizeof(float) * (size_t)W * H);
+    DIS_OMP_ROWS
     for (int y = 0; y < H; ++y) {
         const float* row = src + (size_t)y * W;
         for (int x = 0; x < W; ++x) {
@@ -177,6 +190,7 @@ void dis_oracle_sobel(const float* src, int W, int H, float* dx, float* dy)
             S[(size_t)y * W + x] = c * 0.25f + (l + r) * 0.125f;
         }
     }
+    DIS_OMP_ROWS
     for (int y = 0; y < H; ++y) {
         const size_t ym = (size_t)reflect101(y - 1, H) * W;
         const size_t yc = (size_t)y * W;
@@ -202,7 +216,9 @@ void dis_oracle_pyramid(const float* img, int Wp, int Hp, int coarsest,
             float* gx = (float*)malloc(sizeof(float) * (size_t)W * H);
             float* gy = (float*)malloc(sizeof(float) * (size_t)W * H);
             dis_oracle_sobel(img, W, H, gx, gy);
-            for (size_t i = 0; i < (size_t)W * H; ++i) {
+            const long long npx = (long long)W * H;
+            DIS_OMP_ROWS
+            for (long long i = 0; i < npx; ++i) {
                 float t1 = gx[i] * gx[i];   /* dx.mul(dx)  :21 */
                 float t2 = gy[i] * gy[i];   /* dy.mul(dy)  :22 */
                 float s = t1 + t2;          /* dx2 + dy2   :23 */
@@ -215,6 +231,7 @@ void dis_oracle_pyramid(const float* img, int Wp, int Hp, int coarsest,
              * sum over (sy, sx) in row-major order, times 0.25 */
             const float* p = img_levels + prev_off;
             const int Wq = Wp >> (l - 1);
+            DIS_OMP_ROWS
             for (int y = 0; y < H; ++y)
                 for (int x = 0; x < W; ++x) {
                     const float* a = p + (size_t)(2 * y) * Wq + 2 * x;
@@ -476,23 +493,36 @@ static void densify(const level_ctx* c, int npw, int nph, int steps, int offw, i
     memset(dense, 0, sizeof(float) * 2 * (size_t)W * H);          /* :125 */
     const float half = 0.5f;                                      /* :128 */
     int lb = -c->ps / 2, ub = c->ps / 2 - 1;
-    for (int gx = 0; gx < npw; ++gx)
-        for (int gy = 0; gy < nph; ++gy) {                        /* x-major id order */
-            const int ip = gx * nph + gy;
-            const int rx = gx * steps + offw, ry = gy * steps + offh;
-            const float nu0 = patch_u[2 * ip] * half, nu1 = patch_u[2 * ip + 1] * half;
-            for (int y = lb; y <= ub; ++y)
-                for (int x = lb; x <= ub; ++x) {
-                    int xt = x + rx, yt = y + ry;
-                    if (xt >= 0 && yt >= 0 && xt < W && yt < H) {
-                        size_t i = (size_t)yt * W + xt;
-                        weight[i] = weight[i] + half;
-                        dense[2 * i] = dense[2 * i] + nu0;
-                        dense[2 * i + 1] = dense[2 * i + 1] + nu1;
+    /* row bands [y0, y1): each pixel still receives its patches' terms in
+     * patch-id order (a band walks every patch in id order, writing only its
+     * own rows), so any band count gives the single-threaded result */
+    const int nb = g_threads > 1 ? 4 * g_threads : 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(g_threads) if (g_threads > 1)
+#endif
+    for (int b = 0; b < nb; ++b) {
+        const int y0 = (int)((long long)H * b / nb), y1 = (int)((long long)H * (b + 1) / nb);
+        for (int gx = 0; gx < npw; ++gx)
+            for (int gy = 0; gy < nph; ++gy) {                    /* x-major id order */
+                const int ip = gx * nph + gy;
+                const int rx = gx * steps + offw, ry = gy * steps + offh;
+                if (ry + ub < y0 || ry + lb >= y1) continue;
+                const float nu0 = patch_u[2 * ip] * half, nu1 = patch_u[2 * ip + 1] * half;
+                for (int y = lb; y <= ub; ++y)
+                    for (int x = lb; x <= ub; ++x) {
+                        int xt = x + rx, yt = y + ry;
+                        if (xt >= 0 && yt >= y0 && xt < W && yt < y1) {
+                            size_t i = (size_t)yt * W + xt;
+                            weight[i] = weight[i] + half;
+                            dense[2 * i] = dense[2 * i] + nu0;
+                            dense[2 * i + 1] = dense[2 * i + 1] + nu1;
+                        }
                     }
-                }
-        }
-    for (size_t i = 0; i < (size_t)W * H; ++i)                     /* :138-149 */
+            }
+    }
+    const long long npx = (long long)W * H;
+    DIS_OMP_ROWS
+    for (long long i = 0; i < npx; ++i)                            /* :138-149 */
         if (weight[i] > 0) {
             dense[2 * i] = dense[2 * i] / weight[i];
             dense[2 * i + 1] = dense[2 * i + 1] / weight[i];
@@ -713,10 +743,6 @@ double dis_oracle_var_energy(const float* I0, const float* I1, int stride, int W
     return e;
 }
 
-/* worker threads for the per-level patch loop (1 = the reference's single
- * thread; OpenMP builds only). Test-side speed knob: results are identical. */
-static int g_threads = 1;
-
 int dis_oracle_set_threads(int n)
 {
 #ifdef _OPENMP
@@ -887,6 +913,7 @@ void dis_oracle_upsample_crop(const float* flowF, int Wp, int Hp, int finest,
     /* horizontal pass per source row (HResizeLinear), then vertical
      * (VResizeLinear: S0*b0 + S1*b1, row sy+1 clamped) (:195) */
     float* hrow = (float*)malloc(sizeof(float) * 2 * (size_t)Wp * hF);
+    DIS_OMP_ROWS
     for (int r = 0; r < hF; ++r)
         for (int x = 0; x < Wp; ++x)
             for (int ch = 0; ch < 2; ++ch) {
@@ -896,6 +923,7 @@ void dis_oracle_upsample_crop(const float* flowF, int Wp, int Hp, int finest,
                 else v = S[xi[x] * 2 + ch];
                 hrow[((size_t)r * Wp + x) * 2 + ch] = v;
             }
+    DIS_OMP_ROWS
     for (int y = 0; y < H; ++y) {
         const int yy = y + pad_top;
         const int r0 = yi[yy], r1 = (yi[yy] + 1 < hF) ? yi[yy] + 1 : hF - 1;
@@ -919,6 +947,7 @@ static void pad_plane(const float* src, int W, int H, int pad, int replicate, fl
     /* copyMakeBorder (src/main.cpp:43-47): replicate for the image, zero for
      * the gradients. */
     const int tw = W + 2 * pad, th = H + 2 * pad;
+    DIS_OMP_ROWS
     for (int y = 0; y < th; ++y)
         for (int x = 0; x < tw; ++x) {
             int sx = x - pad, sy = y - pad;
