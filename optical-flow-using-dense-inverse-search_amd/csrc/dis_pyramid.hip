@@ -16,6 +16,8 @@
 // integer Sobel (exact for u8 input), the magnitude sqrtf(N / 64) as
 // sqrt_cr(N) / 8 (correctly rounded), 2x2 means (((a + b) + c) + d) * 0.25
 // with a, b the top row -- bit-identical planes.
+#include <type_traits>
+
 #include "dis_device.h"
 #include "dis_kernels.h"
 
@@ -71,7 +73,8 @@ struct Block4 {
     float l2;        // level 2
 };
 
-__device__ __forceinline__ void block4(const unsigned (&p)[6], const unsigned (&m)[6], const unsigned (&n)[6],
+template <int R0, int NR>
+__device__ __forceinline__ void block4(const unsigned (&p)[NR], const unsigned (&m)[NR], const unsigned (&n)[NR],
                                        Block4& o)
 {
     // rows streamed: X of three window rows live at a time, the magnitudes of
@@ -79,8 +82,9 @@ __device__ __forceinline__ void block4(const unsigned (&p)[6], const unsigned (&
     const short2p cm11 = {-1, 1}, c02 = {0, 2}, c20 = {2, 0}, c1m1 = {1, -1};
     short2p X[3][4];
     auto xrow = [&](int r, short2p (&x)[4]) {
-        const short2p B[6] = {bytes2<3, 3>(p[r], m[r]), bytes2<4, 4>(p[r], m[r]), bytes2<5, 5>(p[r], m[r]),
-                              bytes2<6, 6>(p[r], m[r]), bytes2<7, 7>(p[r], m[r]), bytes2<4, 4>(m[r], n[r])};
+        const unsigned pr = p[R0 + r], mr = m[R0 + r], nr = n[R0 + r];
+        const short2p B[6] = {bytes2<3, 3>(pr, mr), bytes2<4, 4>(pr, mr), bytes2<5, 5>(pr, mr),
+                              bytes2<6, 6>(pr, mr), bytes2<7, 7>(pr, mr), bytes2<4, 4>(mr, nr)};
 #pragma unroll
         for (int c = 0; c < 4; ++c) x[c] = B[c] * cm11 + (B[c + 1] * c02 + B[c + 2]);
     };
@@ -117,19 +121,26 @@ __device__ __forceinline__ void block4(const unsigned (&p)[6], const unsigned (&
     o.l2 = s * 0.25f;
 }
 
-// grid: (ceil(W2 / 256), H2, 2 * batch) waves; z = 2 * pair + frame. Lane =
-// 4 consecutive level-2 pixels of row y2 = level-0 columns x0 .. x0 + 15
-// (x0 = 16 g), window columns x0 - 1 .. x0 + 16, rows 4 y2 - 1 .. 4 y2 + 4.
+// grid: (ceil(W2 / 256), ceil(H2 / RW), 2 * batch) waves; z = 2 * pair +
+// frame. Lane = 4 consecutive level-2 pixels of rows RW y .. RW y + RW - 1 =
+// level-0 columns x0 .. x0 + 15 (x0 = 16 g), window columns x0 - 1 .. x0 + 16,
+// rows 4 RW y - 1 .. 4 RW y + 4 RW: the 2 halo rows are read once per RW
+// level-2 rows (RW 1: 6 rows per 4, 1.5x the frame bytes; RW 2: 1.25x).
 #ifndef DIS_PYR12_XCD
 #define DIS_PYR12_XCD 0  // r03 A/B: HBM bytes 397 -> 300 MB per 32 pairs, but 98 -> 115 us
 #endif
-#ifndef DIS_PYR12_WAVES
-#define DIS_PYR12_WAVES 5  // min waves per SIMD: 91 VGPRs, no spills (6: 80 + 48 B scratch)
+#ifndef DIS_PYR12_ROWS
+#define DIS_PYR12_ROWS 1
 #endif
+#ifndef DIS_PYR12_WAVES
+#define DIS_PYR12_WAVES (DIS_PYR12_ROWS == 1 ? 5 : 4)  // min waves per SIMD (RW 1: 91 VGPRs, no spills)
+#endif
+constexpr int kPyrRW = DIS_PYR12_ROWS;
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12(PyramidArgs a)
 {
+    constexpr int RW = kPyrRW, NR = 4 * RW + 2;
     const int lane = threadIdx.x;
-    const int W2 = a.w[2];
+    const int W2 = a.w[2], H2 = a.Hp >> 2;
 #if DIS_PYR12_XCD
     // XCD-aware wave order (off: measured slower, see the macro): the
     // dispatcher deals linear workgroup ids round-robin to the 8 XCDs; remap
@@ -140,14 +151,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     const int per = nb / 8;
     const int t = lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
     const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
-    const int y2 = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+    const int yb = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
 #else
-    const int bx = blockIdx.x, y2 = blockIdx.y, bz = blockIdx.z;
+    const int bx = blockIdx.x, yb = blockIdx.y, bz = blockIdx.z;
 #endif
+    const int y2b = RW * yb;  // first level-2 row of the wave
     const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
     const int pair = bz >> 1, frame = bz & 1;
-    if (bx == 0 && y2 == 0 && bz == 0 && lane < a.nzero) a.zero[lane] = 0;
+    if (bx == 0 && yb == 0 && bz == 0 && lane < a.nzero) a.zero[lane] = 0;
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
     const int ng = (W2 + 3) >> 2;                 // groups per row
     const int gc = g < ng ? g : ng - 1;           // idle lanes mirror the last group (loads stay in bounds)
@@ -160,21 +172,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     const bool body = a.qword_ok && x0 >= a.pl && x0 + 15 - a.pl <= a.W - 1;
     const bool nb_l = body && lane > 0 && x0 - 16 >= a.pl;
     const bool nb_r = body && lane < 63 && x0 + 31 - a.pl <= a.W - 1 && g + 1 < ng;
-    unsigned d[4][6], wl[6], wr[6];
-    const uint8_t* rows[6];
+    unsigned d[4][NR], wl[NR], wr[NR];
+    const uint8_t* rows[NR];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) rows[r] = in + (size_t)src_row(a, 4 * y2 - 1 + r) * a.stride;
+    for (int r = 0; r < NR; ++r) rows[r] = in + (size_t)src_row(a, 4 * y2b - 1 + r) * a.stride;
     // every row's load in flight before any is consumed (no branch between
     // them): the 16-byte body loads of all lanes (lanes without a body read a
     // harmless in-bounds 16 bytes, W >= 16), then the byte gathers of the
     // lanes that need them (exec-masked, all issued before the wait)
     if (a.qword_ok && a.W >= 16) {
         const int xb = body ? x0 - a.pl : 0;
-        uint4 v[6];
+        uint4 v[NR];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) v[r] = *reinterpret_cast<const uint4*>(rows[r] + xb);
+        for (int r = 0; r < NR; ++r) v[r] = *reinterpret_cast<const uint4*>(rows[r] + xb);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) {
+        for (int r = 0; r < NR; ++r) {
             d[0][r] = v[r].x;
             d[1][r] = v[r].y;
             d[2][r] = v[r].z;
@@ -182,33 +194,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
         }
     }
     if (!body) {  // padding columns, unaligned frames: bytes
-        uint8_t bb[6][16];
+        uint8_t bb[NR][16];
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int k = 0; k < 16; ++k) bb[r][k] = rows[r][src_col(a, x0 + k)];
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 d[k][r] = (unsigned)bb[r][4 * k] | ((unsigned)bb[r][4 * k + 1] << 8) |
                           ((unsigned)bb[r][4 * k + 2] << 16) | ((unsigned)bb[r][4 * k + 3] << 24);
     }
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
+    for (int r = 0; r < NR; ++r) {
         wl[r] = wave_shr1(d[3][r], 0u);
         wr[r] = wave_shl1(d[0][r], 0u);
     }
     if (!nb_l || !nb_r) {  // the wave's end lanes, the plane's edges, the padding
         const int cl = src_col(a, x0 - 1), cr = src_col(a, x0 + 16);
-        uint8_t hl[6], hr[6];
+        uint8_t hl[NR], hr[NR];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) {
+        for (int r = 0; r < NR; ++r) {
             hl[r] = rows[r][cl];
             hr[r] = rows[r][cr];
         }
 #pragma unroll
-        for (int r = 0; r < 6; ++r) {
+        for (int r = 0; r < NR; ++r) {
             if (!nb_l) wl[r] = (unsigned)hl[r] << 24;
             if (!nb_r) wr[r] = (unsigned)hr[r];
         }
@@ -216,46 +228,55 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     if (g >= ng) return;
     float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
     const int np = min(4, W2 - 4 * g);  // level-2 pixels of this lane (the row's last group may be short)
-    float l1row[2][8], l2v[4];
+    auto level_row = [&](auto rr_c) {
+        constexpr int rr = decltype(rr_c)::value;  // level-2 row y2b + rr, window rows 4 rr ..
+        const int y2 = y2b + rr;
+        if (RW > 1 && y2 >= H2) return;
+        float l1row[2][8], l2v[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        Block4 o;
-        block4(q == 0 ? wl : d[q - 1], d[q], q == 3 ? wr : d[q + 1], o);
-        if (a.write_l0 && q < np) {
+        for (int q = 0; q < 4; ++q) {
+            Block4 o;
+            block4<4 * rr, NR>(q == 0 ? wl : d[q - 1], d[q], q == 3 ? wr : d[q + 1], o);
+            if (a.write_l0 && q < np) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                *reinterpret_cast<float4*>(planes + (size_t)(4 * y2 + r) * a.Wp + x0 + 4 * q) =
-                    make_float4(o.m[r][0] * 0.125f, o.m[r][1] * 0.125f, o.m[r][2] * 0.125f, o.m[r][3] * 0.125f);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            l1row[i][2 * q] = o.l1[i][0];
-            l1row[i][2 * q + 1] = o.l1[i][1];
-        }
-        l2v[q] = o.l2;
-    }
-    float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 8 * g;
-    float* p2 = planes + a.off[2] + (size_t)y2 * W2 + 4 * g;
-    if (np == 4) {  // 16-byte stores (level-1 rows and the level-2 plane are 16-byte aligned: W % 16 == 0 here)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1]) =
-                make_float4(l1row[i][0], l1row[i][1], l1row[i][2], l1row[i][3]);
-            *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1] + 4) =
-                make_float4(l1row[i][4], l1row[i][5], l1row[i][6], l1row[i][7]);
-        }
-        *reinterpret_cast<float4*>(p2) = make_float4(l2v[0], l2v[1], l2v[2], l2v[3]);
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (q < np) {
-                p1[2 * q] = l1row[0][2 * q];
-                p1[2 * q + 1] = l1row[0][2 * q + 1];
-                p1[a.w[1] + 2 * q] = l1row[1][2 * q];
-                p1[a.w[1] + 2 * q + 1] = l1row[1][2 * q + 1];
-                p2[q] = l2v[q];
+                for (int r = 0; r < 4; ++r)
+                    *reinterpret_cast<float4*>(planes + (size_t)(4 * y2 + r) * a.Wp + x0 + 4 * q) =
+                        make_float4(o.m[r][0] * 0.125f, o.m[r][1] * 0.125f, o.m[r][2] * 0.125f, o.m[r][3] * 0.125f);
             }
-    }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                l1row[i][2 * q] = o.l1[i][0];
+                l1row[i][2 * q + 1] = o.l1[i][1];
+            }
+            l2v[q] = o.l2;
+        }
+        float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 8 * g;
+        float* p2 = planes + a.off[2] + (size_t)y2 * W2 + 4 * g;
+        if (np == 4) {  // 16-byte stores (level-1 rows and the level-2 plane are 16-byte aligned: W % 16 == 0 here)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1]) =
+                    make_float4(l1row[i][0], l1row[i][1], l1row[i][2], l1row[i][3]);
+                *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1] + 4) =
+                    make_float4(l1row[i][4], l1row[i][5], l1row[i][6], l1row[i][7]);
+            }
+            *reinterpret_cast<float4*>(p2) = make_float4(l2v[0], l2v[1], l2v[2], l2v[3]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < np) {
+                    p1[2 * q] = l1row[0][2 * q];
+                    p1[2 * q + 1] = l1row[0][2 * q + 1];
+                    p1[a.w[1] + 2 * q] = l1row[1][2 * q];
+                    p1[a.w[1] + 2 * q + 1] = l1row[1][2 * q + 1];
+                    p2[q] = l2v[q];
+                }
+        }
+    };
+    level_row(std::integral_constant<int, 0>{});
+    if constexpr (RW > 1) level_row(std::integral_constant<int, 1>{});
+    if constexpr (RW > 2) level_row(std::integral_constant<int, 2>{});
+    if constexpr (RW > 3) level_row(std::integral_constant<int, 3>{});
 }
 
 // grid: (W2 / T2, H2 / T2, 2 * batch), T2 = 2^(L-2) level-2 pixels per tile
@@ -310,7 +331,7 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     if (!pyramid2_fits(a) || a.nzero > 64) return hipErrorInvalidValue;
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
-    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, H2, 2 * batch), dim3(64), 0, s, a);
+    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (H2 + kPyrRW - 1) / kPyrRW, 2 * batch), dim3(64), 0, s, a);
     if (a.levels >= 3) {
         const int T2 = 1 << (a.levels - 2);
         const dim3 grid(W2 / T2, H2 / T2, 2 * batch);
