@@ -48,6 +48,12 @@
 #ifndef DIS_LOOP_SELECT
 #define DIS_LOOP_SELECT 1
 #endif
+#ifndef DIS_SPLIT_PATCH
+#define DIS_SPLIT_PATCH 1  // LPP 2: per-patch scalar work split between the patch's two lanes
+#endif
+#ifndef DIS_SPLIT_FENCE
+#define DIS_SPLIT_FENCE false  // sched fence per tap row: 124 VGPRs, measured -1.2 % (r03 A/B)
+#endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
 #endif
@@ -381,6 +387,89 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
     *pu1 = u1;
 }
 
+[[maybe_unused]] __device__ __forceinline__ float xor1f(float v) { return quad_perm<kQuadXor1>(v); }
+[[maybe_unused]] __device__ __forceinline__ int xor1i(int v) { return __builtin_amdgcn_mov_dpp(v, kQuadXor1, 0xF, 0xF, true); }
+
+// The LPP-2 iteration with the per-patch scalar work split between the
+// patch's two lanes (lanes 2k, 2k+1; partner = lane ^ 1): lane q carries
+// coordinate q of the patch (0: x, 1: y) -- its reference, start and current
+// position, its floor / fraction / ceil in the warp, its part of the tap base,
+// its displacement and its bounds test -- so one instruction serves both
+// coordinates, and the two right-hand sides come out one per lane from a
+// single cross-lane stage: lane 0 holds (g1, g2) = (gx, gy), lane 1 (gy, gx),
+// so C_ci = A_ci(g1) + partner's A_ci(g2) is b0's column sum on lane 0 and
+// b1's on lane 1. Every value is the one iterate() computes: the cross-lane
+// products and sums pair the same operands (IEEE mul and add commute), the
+// solve runs on both lanes from the same (c0, c1). `tap_at(cv)` gets the lane's
+// own ceil coordinate.
+template <bool kFence, bool kPaper, bool kFma, typename TapAt>
+__device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& lu, const float (&g1)[32],
+                                              const float (&g2)[32], int q, float rv, float iv, float btv,
+                                              float* puv, TapAt&& tap_at)
+{
+    auto mac = [](float acc, float x, float y) { return kFma ? __builtin_fmaf(x, y, acc) : acc + x * y; };
+    float uv = iv;
+    const float sv = rv + uv;
+    float pv = sv;
+    const float ubv = q ? a.tmp_ub_h : a.tmp_ub_w;
+    const bool f = (lu.swap != 0) != (q != 0);  // c0 takes the partner's right-hand side
+    float r[32];
+    const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;  // div_pre
+    for (int counter = 1;; ++counter) {
+        // warp_coefs, one coordinate per lane: a (b) = frac, 1 - a (1 - b)
+        const float fl = floorf(pv), fr = pv - fl, om = 1 - fr;
+        const int cv = (int)ceilf(pv + .00001f);
+        const float s1 = q ? om : fr, s2w = q ? fr : om;
+        Warp w;
+        w.w0 = xor1f(om) * om;    // (1 - a)(1 - b)
+        w.w1 = xor1f(s1) * s1;    // a (1 - b)
+        w.w2 = xor1f(s2w) * s2w;  // b (1 - a)
+        w.w3 = xor1f(fr) * fr;    // a b
+        warp_patch<2, kFence, kFma>(w, a.norm, tap_at(cv), r);
+        float C[4];
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            float x = g1[8 * ci] * r[8 * ci], y = g2[8 * ci] * r[8 * ci];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) {
+                x = mac(x, g1[8 * ci + j], r[8 * ci + j]);
+                y = mac(y, g2[8 * ci + j], r[8 * ci + j]);
+            }
+            C[ci] = x + xor1f(y);
+        }
+        float bown = (C[0] + C[2]) + (C[1] + C[3]);  // lane 0: b0, lane 1: b1
+        if constexpr (kPaper) bown = bown - btv;
+        const float bpart = xor1f(bown);
+        float d0, c1;
+        {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
+            float c0 = f ? bpart : bown;
+            c1 = f ? bown : bpart;
+            c1 = c1 - lu.l10 * c0;
+            if constexpr (kFma) {
+                c1 = c1 * r11;
+                c0 = __builtin_fmaf(-c1, lu.u01, c0);
+                d0 = c0 * r00;
+            } else {
+                c1 = div_pre(c1, lu.u11, r11);
+                c0 = c0 - c1 * lu.u01;
+                d0 = div_pre(c0, lu.u00, r00);
+            }
+        }
+        uv = uv - (q ? c1 : d0);
+        pv = rv + uv;
+        const float ev = sv - pv, e2 = ev * ev;
+        const float n2 = e2 + xor1f(e2);  // ex * ex + ey * ey
+        const bool bad_own = n2 > a.thr_sq || n2 != n2 || pv < a.tmp_lb || pv > ubv;
+        // either coordinate out: the pair's OR, on the scalar unit
+        unsigned long long m = __builtin_amdgcn_ballot_w64(bad_own);
+        m |= ((m >> 1) & 0x5555555555555555ull) | ((m << 1) & 0xAAAAAAAAAAAAAAAAull);
+        const bool bad = __builtin_amdgcn_inverse_ballot_w64(m);
+        uv = bad ? iv : uv;
+        if (bad || counter > a.iters) break;
+    }
+    *puv = uv;
+}
+
 }  // namespace
 
 #ifndef DIS_XCD_REMAP
@@ -651,6 +740,16 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         const float h11 = patch_dot<LPP, kFma>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
+    // LPP 2, split iteration (iterate_split): the y lane keeps (gy, gx)
+    constexpr bool kSplit = LPP == 2 && DIS_SPLIT_PATCH && !kPhys;
+    if constexpr (kSplit) {
+#pragma unroll
+        for (int j = 0; j < 8 * NC; ++j) {
+            const float x = gdx[j], y = gdy[j];
+            gdx[j] = q ? y : x;
+            gdy[j] = q ? x : y;
+        }
+    }
     const float sx = rx + ix, sy = ry + iy;
     const bool valid = active && !(sx < a.tmp_lb || sy < a.tmp_lb || sx > a.tmp_ub_w || sy > a.tmp_ub_h);
 
@@ -681,6 +780,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int TS = TSC ? TSC : a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
 
     float u0 = ix, u1 = iy;
+    float uv = q ? iy : ix;  // split iteration: the lane's coordinate
     if (use_tile) {
         // 64-column strips; rows in groups of kTileGroup per wave (loads in
         // flight, then the LDS stores)
@@ -706,7 +806,31 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             }
         }
         __syncthreads();
-        if (valid) {
+        if constexpr (kSplit) {
+            if (valid) {
+                // lane's part of the tap base (tile + (Y-5-ty0) TS + (X-5+qb-tx0)):
+                // x lane (X - 5 - tx0), y lane (Y - 5 - ty0) TS; summed with the
+                // partner's by one DPP add
+                const int M = q ? TS : 1, K = q ? -(5 + ty0) * TS : -(5 + tx0);
+                const float* tq = tile + 4 * q;
+                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, q ? bt1 : bt0, &uv,
+                                                   [&](int cv) {
+                                                       const int t = __mul24(cv, M) + K;
+                                                       // three row groups, each one base register and
+                                                       // ds_read2 immediates (<= 255 dwords); opaque to the
+                                                       // compiler, which otherwise re-adds a base per pair
+                                                       const int o0 = t + xor1i(t);
+                                                       int o1 = o0 + 3 * TS, o2 = o0 + 6 * TS;
+                                                       __asm__("" : "+v"(o1));
+                                                       __asm__("" : "+v"(o2));
+                                                       const float *b0 = tq + o0, *b1 = tq + o1, *b2 = tq + o2;
+                                                       return [=](int k, int c) {
+                                                           return k < 3 ? b0[k * TS + c]
+                                                                        : k < 6 ? b1[(k - 3) * TS + c] : b2[(k - 6) * TS + c];
+                                                       };
+                                                   });
+            }
+        } else if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
             iterate<LPP, false, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
 #ifdef DIS_EXP_TAPBANKS  // experiment: lane-fixed, conflict-free tap addresses (wrong values)
@@ -718,7 +842,19 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             });
         }
     } else if constexpr (kFallback) {
-        if (valid) {
+        if constexpr (kSplit) {
+            if (valid) {
+                iterate_split<true, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, q ? bt1 : bt0, &uv,
+                                                  [&](int cv) {
+                                                      const int cp = xor1i(cv);
+                                                      const int y0 = (q ? cv : cp) - 5, x0 = (q ? cp : cv) - 5 + 4 * q;
+                                                      return [=](int k, int c) {
+                                                          return I1[(ptrdiff_t)clampi(y0 + k, lo, H - 1 + pad) * ld +
+                                                                    clampi(x0 + c, lo, W - 1 + pad)];
+                                                      };
+                                                  });
+            }
+        } else if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
             iterate<LPP, true, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
                 const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
@@ -734,6 +870,11 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             a.fb_list[slot] = (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi;
         }
         return;
+    }
+    if constexpr (kSplit) {  // every lane (reconverged): the partner's coordinate
+        const float up = xor1f(uv);
+        u0 = q ? up : uv;
+        u1 = q ? uv : up;
     }
     if (active && q == 0) a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
 }
