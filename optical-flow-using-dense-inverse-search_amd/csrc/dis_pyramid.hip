@@ -129,6 +129,9 @@ __device__ __forceinline__ void block4(const unsigned (&p)[NR], const unsigned (
 #ifndef DIS_PYR12_XCD
 #define DIS_PYR12_XCD 0  // r03 A/B: HBM bytes 397 -> 300 MB per 32 pairs, but 98 -> 115 us
 #endif
+#ifndef DIS_PYR12_CHUNK
+#define DIS_PYR12_CHUNK 8  // DIS_PYR12_XCD 2: level-2 rows per XCD chunk
+#endif
 #ifndef DIS_PYR12_ROWS
 #define DIS_PYR12_ROWS 1
 #endif
@@ -148,8 +151,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     // a wave shares with the next row's wave are read from HBM once
     const int nbx = gridDim.x, nby = gridDim.y, nb = nbx * nby * gridDim.z;
     const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+#if DIS_PYR12_XCD == 2
+    // chunked: XCD k takes chunks of CH consecutive waves (DIS_PYR12_CHUNK
+    // rows x the row's waves), the 8 XCDs neighbouring chunks, so the waves in
+    // flight still cover one compact band of the frames (DRAM locality of the
+    // plain order) while vertically adjacent waves mostly share an L2
+    const int CH = DIS_PYR12_CHUNK * nbx, grp = 8 * CH;
+    const int j = lin >> 3, k = lin & 7;
+    const int t = lin < nb / grp * grp ? (j / CH) * grp + k * CH + j % CH : lin;
+#else
     const int per = nb / 8;
     const int t = lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
+#endif
     const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
     const int yb = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
