@@ -530,6 +530,19 @@ __device__ __forceinline__ void out_rows_f1(const OutputArgs& a, const float2* d
 // K = ceil(ps / steps) bounds the covering patches per axis, so the gather is
 // an unrolled, predicated K x K loop (no divergent loops).
 template <bool UPSAMPLE, int K, bool kPaper = false>
+#ifdef DIS_STAMP  // diagnostic: every workgroup's end clock, max per call (see kStampN)
+#define OUT_STAMP()                                                                                   \
+    do {                                                                                              \
+        if (a.stamp && threadIdx.x == 0) {                                                            \
+            const unsigned long long n = __hip_atomic_load(&a.stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+            atomicMax(&a.stamp[1 + kStampN + ((n - 1) % kStampN)], wall_clock64());                   \
+        }                                                                                             \
+    } while (0)
+#else
+#define OUT_STAMP() \
+    do {            \
+    } while (0)
+#endif
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
     constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
@@ -682,6 +695,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                 case 2: out_rows_f1<1, 0, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
                 default: out_rows_f1<1, 1, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
             }
+            OUT_STAMP();
             return;
         }
     }
@@ -745,6 +759,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             dst[0] = o[0];
         }
     }
+    OUT_STAMP();
 }
 
 bool output_fits(const OutputArgs& a)

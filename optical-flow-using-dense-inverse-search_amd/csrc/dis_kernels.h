@@ -130,6 +130,7 @@ struct PyramidArgs {
     int nzero;
     int dword_ok;               // I0/I1, stride, pair_stride and pad_left 4-byte aligned: dword row loads
     int qword_ok;               // ... and 16-byte aligned, pad_left a multiple of 16: 16-byte row loads
+    unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call start clocks, else null
 };
 
 // Fused densify + upsample + crop (dis_frontback.hip).
@@ -146,7 +147,12 @@ struct OutputArgs {
     const float* img0;  // level-F planes of pair 0 (pre-offset), pair stride plane_stride
     const float* img1;
     long long plane_stride;
+    unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call end clocks, else null
 };
+
+// DIS_STAMP layout per sub-batch stream: [0] call counter, [1 .. kStampN]
+// k_pyr12 start clocks, [1 + kStampN .. 2 kStampN] k_output end clocks (s_memrealtime, 100 MHz)
+constexpr int kStampN = 4096;
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t = {});
 // the same planes by two streaming kernels (dis_pyramid.hip): levels 1-2 from

@@ -173,6 +173,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
     const int pair = bz >> 1, frame = bz & 1;
     if (bx == 0 && yb == 0 && bz == 0 && lane < a.nzero) a.zero[lane] = 0;
+#ifdef DIS_STAMP
+    if (a.stamp && bx == 0 && yb == 0 && bz == 0 && lane == 0) {
+        const unsigned long long n = atomicAdd(&a.stamp[0], 1ull);
+        a.stamp[1 + (n % kStampN)] = wall_clock64();
+    }
+#endif
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
     const int ng = (W2 + 3) >> 2;                 // groups per row
     const int gc = g < ng ? g : ng - 1;           // idle lanes mirror the last group (loads stay in bounds)

@@ -148,6 +148,7 @@ struct dis_ctx {
     static constexpr int kMaxSub = 8;
     int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
     int precision = 0;                   // dis_set_precision: DIS_PRECISION_EXACT / _FMA
+    unsigned long long* stamp = nullptr;  // DIS_STAMP diagnostic builds: per-sub-batch call clocks
     hipStream_t sub[kMaxSub] = {};
     hipEvent_t fork = nullptr;
     // end of the previous call's work on its stream: every call first orders
@@ -257,6 +258,7 @@ dis_status check_params(const dis_params* p, int W, int H)
 
 void free_ws(dis_ctx* c)
 {
+    hipFree(c->stamp);
     hipFree(c->img0);
     hipFree(c->img1);
     hipFree(c->dx);
@@ -471,6 +473,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
             pa.zero = fb_count;
             pa.nzero = g.C + 1;
+            pa.stamp = c->stamp ? c->stamp + (size_t)sub * (1 + 2 * dis::kStampN) : nullptr;
             pa.dword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
                             (n > 1 ? pair_stride : 0) | (size_t)g.pad_left) & 3) == 0;
             pa.qword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
@@ -671,6 +674,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         o.img0 = img0 + LF.plane_off;
         o.img1 = img1 + LF.plane_off;
         o.plane_stride = g.plane_stride;
+        o.stamp = c->stamp ? c->stamp + (size_t)sub * (1 + 2 * dis::kStampN) : nullptr;
         fused_out = dis::output_fits(o) && !vr;  // refined: the finest dense field exists
     }
     if (fused_out) {
@@ -1136,6 +1140,12 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
         ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
              hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess;
     }
+#ifdef DIS_STAMP  // diagnostic builds: per-call clocks of each sub-batch stream (tools/stamp_probe.py)
+    if (ok && getenv("DIS_STAMP")) {
+        const size_t ns = sizeof(unsigned long long) * dis_ctx::kMaxSub * (1 + 2 * dis::kStampN);
+        ok = hipMalloc(&c->stamp, ns) == hipSuccess && hipMemset(c->stamp, 0, ns) == hipSuccess;
+    }
+#endif
     if (ok && params->var_refine_iters > 0) {
         c->vr_plane = (long long)g.lv[g.F].W * g.lv[g.F].H;  // the largest refined level
         ok = hipMalloc(&c->vr_ws, sizeof(float) * dis::kVarRefPlanes * c->vr_plane * B) == hipSuccess;
@@ -1573,5 +1583,19 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     hipFree(maxbits);
     return rc;
 }
+
+#ifdef DIS_STAMP
+// diagnostic builds only (not in include/dis_abi.h): copy the stamp buffer
+int dis_stamp_read(dis_ctx* c, unsigned long long* host, size_t n)
+{
+    if (!c || !c->stamp || !host) return -1;
+    hipSetDevice(c->device);
+    const size_t ns = (size_t)dis_ctx::kMaxSub * (1 + 2 * dis::kStampN);
+    return hipMemcpy(host, c->stamp, sizeof(unsigned long long) * std::min(n, ns), hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#endif
 
 }  // extern "C"
