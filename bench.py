@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="process group backend for N > 1 (nccl = RCCL; "
                     "gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch events")
+    ap.add_argument("--default-stream", action="store_true", help="diagnostic: issue the calls on the default stream")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="skip the extra two-batches-in-flight measurement (reported beside, never as, value)")
     ap.add_argument("--no-tolerance-mode", action="store_true",
@@ -251,7 +252,11 @@ def main():
     eng = disflow.DenseInverseSearch(params, W, H, max_batch=B, device=local)
     if a.streams:
         eng.set_concurrency(a.streams)
-    stream = torch.cuda.current_stream(dev)
+    # the calls go to a dedicated stream: HIP's null (default) stream carries
+    # implicit synchronisation with the device's other streams (measured: the
+    # two-context pattern below lost 7 % on it)
+    stream = torch.cuda.current_stream(dev) if a.default_stream else torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)  # inputs uploaded on the default stream are complete
 
     def step():
         eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), stream.cuda_stream)
@@ -317,24 +322,30 @@ def main():
                     "note": "torch device copy (read+write bytes) and fill of 1 GiB, 10 reps"}
         del x, y
     # Serving pattern: two batches in flight -- steps issued
-    # alternately to two contexts on two streams (one sub-batch stream each),
-    # so one batch's latency-bound coarse levels and output overlap the other's
-    # search. Same K steps of B pairs, every flow written; reported beside
-    # `value` (which keeps one batch at a time on one stream).
+    # alternately to two contexts on two caller streams, one sub-batch stream
+    # each, both replaying their graphs: no fork/join per call, and each
+    # context's gap between calls is filled by the other's work. Same K steps
+    # of B pairs, every flow written; reported beside `value` (which keeps one
+    # batch at a time on one stream). (Linking the two contexts with
+    # dis_pipeline_link forces eager enqueue: measured slower)
     piped = None
     if not a.no_pipelined:
         engs = [eng, disflow.DenseInverseSearch(params, W, H, max_batch=B, device=local)]
-        strs = [stream, torch.cuda.Stream(dev)]
+        strs = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]  # not the default stream (implicit syncs)
         out2 = torch.empty_like(out)
         outs2 = [out, out2]
         for e in engs:
             e.set_concurrency(1)
-        engs[0].pipeline_link(engs[1])  # one batch's head beside the other's body
 
         def pstep(k):
             engs[k % 2].calc_device(B, d0.data_ptr(), d1.data_ptr(), outs2[k % 2].data_ptr(), strs[k % 2].cuda_stream)
-        for k in range(max(2, a.warmup // 2)):
+        t_w = time.perf_counter()
+        k = 0
+        while k < max(2, a.warmup) or time.perf_counter() - t_w < a.warmup_floor:
             pstep(k)
+            k += 1
+            if k % 8 == 0:
+                torch.cuda.synchronize(dev)
         torch.cuda.synchronize(dev)
         barrier()
         torch.cuda.synchronize(dev)
@@ -348,14 +359,14 @@ def main():
         if world > 1:
             torch.distributed.all_reduce(el_p, op=torch.distributed.ReduceOp.MAX)
         same = bool(torch.equal(out2.view(torch.int32), out.view(torch.int32)))
-        engs[0].pipeline_link(None)
         engs[1].close()
         del out2
         eng.set_concurrency(a.streams if a.streams else 2)
         piped = {"inflight": 2, "value": world * B * a.steps / float(el_p.item()), "unit": "frame-pairs/s",
                  "ms_per_step": float(el_p.item()) / a.steps * 1e3, "outputs_identical": same,
-                 "note": "same K steps of B pairs per GPU, issued alternately to two contexts on two streams "
-                         "(one sub-batch stream each); every flow computed and written"}
+                 "note": "same K steps of B pairs per GPU, issued alternately to two contexts on two caller "
+                         "streams (one sub-batch stream each, graphs replayed, no link); every flow computed "
+                         "and written"}
 
     # DIS_PRECISION_FMA (opt-in tolerance mode): the same steps
     # timed the same way after the headline measurement, its finest launch

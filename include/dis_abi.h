@@ -193,7 +193,9 @@ dis_status dis_set_precision(dis_ctx* ctx, int mode);
  * reached its VALU-bound levels (the search of level F+1), so one batch's head
  * runs beside the other's body instead of beside the other's head; each
  * context still orders its own calls on its workspace as usual. Linked calls
- * are enqueued eagerly (no graph replay). Results do not depend on it.
+ * are enqueued eagerly (no graph replay), which costs more than the gating
+ * gains: for throughput, leave two engines unlinked on two dedicated streams
+ * (INTEGRATION.md). Results do not depend on it.
  * b == NULL unlinks a (and its peer); linking replaces earlier links of both. */
 dis_status dis_pipeline_link(dis_ctx* a, dis_ctx* b);
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
