@@ -300,41 +300,60 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
 
 // grid: (W2 / T2, H2 / T2, 2 * batch), T2 = 2^(L-2) level-2 pixels per tile
 // edge; one wave per tile computes levels 3..L in LDS
-template <int L>
+#ifndef DIS_TAIL_TPW
+#define DIS_TAIL_TPW 2  // level-2 tiles per wave, loads in flight together (r03: 1 / 2 / 3 / 5 -> 20.2 / 14.0 / 16.1 / 16.8 us)
+#endif
+template <int L, int TPW>
 __global__ void __launch_bounds__(64) k_pyr_tail(PyramidArgs a)
 {
     constexpr int T2 = 1 << (L - 2), N2 = T2 * T2;
     constexpr int PER = (N2 + 63) / 64;
-    __shared__ float buf[2][N2 / 4];  // level l at buf[l & 1]
-    __shared__ float src[N2];         // the level-2 tile
+    constexpr int NB = N2 / 4 > 0 ? N2 / 4 : 1;
+    __shared__ float buf[TPW][2][NB];  // level l of tile t at buf[t][l & 1]
+    __shared__ float src[TPW][N2];     // the level-2 tiles
     const int lane = threadIdx.x;
     const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
     float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
-    const int tx = blockIdx.x * T2, ty = blockIdx.y * T2;  // level-2 tile origin
-    const float* p2 = planes + a.off[2] + (size_t)ty * a.w[2] + tx;
+    const int ntx = a.w[2] / T2;                              // tiles per tile row
+    const int t0 = blockIdx.x * TPW, ty = blockIdx.y * T2;   // first tile, level-2 row origin
+    const float* p2 = planes + a.off[2] + (size_t)ty * a.w[2];
+    float v[TPW][PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int i = lane + 64 * k;
-        if (i < N2) src[i] = p2[(size_t)(i / T2) * a.w[2] + (i % T2)];
-    }
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = lane + 64 * k;
+            v[t][k] = (t0 + t < ntx && i < N2) ? p2[(size_t)(i / T2) * a.w[2] + (t0 + t) * T2 + (i % T2)] : 0.0f;
+        }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = lane + 64 * k;
+            if (i < N2) src[t][i] = v[t][k];
+        }
     __syncthreads();
-    const float* cur = src;
 #pragma unroll
     for (int l = 3; l <= L; ++l) {
         const int ns = T2 >> (l - 3), nd = ns / 2;
-        float* nxt = buf[l & 1];
-        for (int k = lane; k < nd * nd; k += 64) {
-            const int y = k / nd, x = k - y * nd;
-            const float* p = cur + (2 * y) * ns + 2 * x;
-            float s = p[0] + p[1];
-            s = s + p[ns];
-            s = s + p[ns + 1];
-            const float v = s * 0.25f;
-            nxt[k] = v;
-            planes[a.off[l] + (size_t)((ty >> (l - 2)) + y) * a.w[l] + (tx >> (l - 2)) + x] = v;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            if (t0 + t >= ntx) break;  // uniform
+            const float* cur = l == 3 ? src[t] : buf[t][(l - 1) & 1];
+            float* nxt = buf[t][l & 1];
+            const int tx = (t0 + t) * T2;
+            for (int k = lane; k < nd * nd; k += 64) {
+                const int y = k / nd, x = k - y * nd;
+                const float* p = cur + (2 * y) * ns + 2 * x;
+                float s = p[0] + p[1];
+                s = s + p[ns];
+                s = s + p[ns + 1];
+                const float val = s * 0.25f;
+                nxt[k] = val;
+                planes[a.off[l] + (size_t)((ty >> (l - 2)) + y) * a.w[l] + (tx >> (l - 2)) + x] = val;
+            }
         }
         __syncthreads();
-        cur = nxt;
     }
 }
 
@@ -352,13 +371,13 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     if (a.w[2] != W2) return hipErrorInvalidValue;
     DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (H2 + kPyrRW - 1) / kPyrRW, 2 * batch), dim3(64), 0, s, a);
     if (a.levels >= 3) {
-        const int T2 = 1 << (a.levels - 2);
-        const dim3 grid(W2 / T2, H2 / T2, 2 * batch);
+        const int T2 = 1 << (a.levels - 2), TPW = DIS_TAIL_TPW;
+        const dim3 grid((W2 / T2 + TPW - 1) / TPW, H2 / T2, 2 * batch);
         switch (a.levels) {
-            case 3: hipLaunchKernelGGL(k_pyr_tail<3>, grid, dim3(64), 0, s, a); break;
-            case 4: hipLaunchKernelGGL(k_pyr_tail<4>, grid, dim3(64), 0, s, a); break;
-            case 5: hipLaunchKernelGGL(k_pyr_tail<5>, grid, dim3(64), 0, s, a); break;
-            default: hipLaunchKernelGGL(k_pyr_tail<6>, grid, dim3(64), 0, s, a); break;
+            case 3: hipLaunchKernelGGL((k_pyr_tail<3, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
+            case 4: hipLaunchKernelGGL((k_pyr_tail<4, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
+            case 5: hipLaunchKernelGGL((k_pyr_tail<5, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_pyr_tail<6, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
         }
     }
     return hipGetLastError();
