@@ -121,11 +121,25 @@ __device__ __forceinline__ float2 dense_at(const float2* __restrict__ u, int npw
 // Correctly rounded sqrt for x = 0 or a normal float well inside the range
 // (no denormal pre-scaling): v_sqrt_f32 is within one ulp; the fma residuals
 // of the neighbours r -/+ 1 ulp pick the rounded root. Used by the pyramid on
-// x = N, an integer < 2^22 (Sobel magnitude^2 * 64); tools/sqrt_check proves
-// it equal to sqrtf on every such N on gfx950 (the raw v_sqrt_f32 is not).
+// x = N, an integer < 2^22 (Sobel magnitude^2 * 64). On that domain the raw
+// v_sqrt_f32 of gfx950 is either RN(sqrt N) or one ulp BELOW it (never above:
+// tools/sqrt_dir, all 2,080,801 N: 1,744,787 exact, 336,014 one ulp low), so
+// only the round-up test is needed (DIS_SQRT_SIDE 1, the default: 4 VALU
+// instead of 8; k_pyr12 98.7 -> 85.4 us per 32 1080p pairs). tools/sqrt_check
+// (a -m gpu test) proves the compiled form equal to sqrtf on every such N.
+#ifndef DIS_SQRT_SIDE
+#define DIS_SQRT_SIDE 1  // 0: both tests; 1 / 2: only the round-up / round-down test
+#endif
 __device__ __forceinline__ float sqrt_cr(float x)
 {
     const float r = __builtin_amdgcn_sqrtf(x);
+    if constexpr (DIS_SQRT_SIDE == 1) {
+        const float rp = __int_as_float(__float_as_int(r) + 1);
+        return __builtin_fmaf(-rp, r, x) > 0.0f ? rp : r;
+    } else if constexpr (DIS_SQRT_SIDE == 2) {
+        const float rm = __int_as_float(__float_as_int(r) - 1);
+        return __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
+    }
     const float rm = __int_as_float(__float_as_int(r) - 1);
     const float rp = __int_as_float(__float_as_int(r) + 1);
     const float em = __builtin_fmaf(-rm, r, x);
