@@ -138,11 +138,14 @@ __device__ __forceinline__ void block4(const unsigned (&p)[NR], const unsigned (
 #ifndef DIS_PYR12_WAVES
 #define DIS_PYR12_WAVES (DIS_PYR12_ROWS == 1 ? 5 : 4)  // min waves per SIMD (RW 1: 91 VGPRs, no spills)
 #endif
-constexpr int kPyrRW = DIS_PYR12_ROWS;
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12(PyramidArgs a)
+#ifndef DIS_PYR12_WG
+#define DIS_PYR12_WG 1  // waves per workgroup, stacked vertically (same CU: the shared halo rows hit in L1/L2)
+#endif
+constexpr int kPyrRW = DIS_PYR12_ROWS, kPyrWG = DIS_PYR12_WG;
+__global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12(PyramidArgs a)
 {
     constexpr int RW = kPyrRW, NR = 4 * RW + 2;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int W2 = a.w[2], H2 = a.Hp >> 2;
 #if DIS_PYR12_XCD
     // XCD-aware wave order (off: measured slower, see the macro): the
@@ -167,7 +170,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR
     const int yb = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
 #else
-    const int bx = blockIdx.x, yb = blockIdx.y, bz = blockIdx.z;
+    const int bx = blockIdx.x, bz = blockIdx.z;
+    const int yb = kPyrWG == 1 ? blockIdx.y : blockIdx.y * kPyrWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (kPyrWG > 1 && RW * yb >= H2) return;
 #endif
     const int y2b = RW * yb;  // first level-2 row of the wave
     const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
@@ -357,6 +362,86 @@ __global__ void __launch_bounds__(64) k_pyr_tail(PyramidArgs a)
     }
 }
 
+// k_pyr_tail_reg<L, TPW>: the same levels 3..L without LDS or barriers. One
+// wave per TPW horizontally adjacent 16 x 16 level-2 super-tiles; lane
+// (qx, qy) = (lane & 7, lane >> 3) loads its 2 x 2 level-2 quad (two 8-byte
+// loads) and forms its level-3 pixel in-lane; level 4 / 5 / 6 take the 2 x 2
+// of the level below from the lanes 1 / 2 / 4 columns and 8 / 16 / 32 lanes
+// away (DPP quad_perm and row_ror:8, ds_bpermute for the rest) -- the same
+// ((a + b) + c) + d, a, b the top row, as k_pyr_tail, so bit-identical planes.
+// Edge super-tiles (level-2 planes not a multiple of 16 wide / high, L < 6)
+// load 0 outside the plane and store only in-plane pixels, whose sources are
+// all in-plane (W_l = W_2 / 2^(l-2) exactly: pyramid2_fits).
+namespace {
+template <int X>
+__device__ __forceinline__ float lane_xor(float v)
+{
+    if constexpr (X == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+    else if constexpr (X == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+    else if constexpr (X == 8) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true));
+    else return __shfl_xor(v, X);
+}
+// 2x2 mean of the level below held at lanes (+0, +DX, +DY, +DX+DY); valid at the top-left lane
+template <int DX, int DY>
+__device__ __forceinline__ float quad_mean(float v)
+{
+    const float tr = lane_xor<DX>(v);  // every lane: its x partner's value
+    const float bl = lane_xor<DY>(v);
+    const float br = lane_xor<DY>(tr);
+    float s = v + tr;
+    s = s + bl;
+    s = s + br;
+    return s * 0.25f;
+}
+}  // namespace
+
+template <int L, int TPW>
+__global__ void __launch_bounds__(64) k_pyr_tail_reg(PyramidArgs a)
+{
+    const int lane = threadIdx.x, qx = lane & 7, qy = lane >> 3;
+    const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
+    float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
+    const int W2 = a.w[2], H2 = a.Hp >> 2;
+    const int y2 = 16 * blockIdx.y + 2 * qy;  // lane's level-2 rows y2, y2 + 1
+    const float* p2 = planes + a.off[2];
+    float2 top[TPW], bot[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int x2 = 16 * (blockIdx.x * TPW + t) + 2 * qx;
+        const bool in = x2 < W2 && y2 < H2;  // W2, H2 even: the whole quad is in or out
+        top[t] = in ? *reinterpret_cast<const float2*>(p2 + (size_t)y2 * W2 + x2) : make_float2(0.0f, 0.0f);
+        bot[t] = in ? *reinterpret_cast<const float2*>(p2 + (size_t)(y2 + 1) * W2 + x2) : make_float2(0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int sx = blockIdx.x * TPW + t;  // super-tile column
+        // level 3: in-lane
+        float s = top[t].x + top[t].y;
+        s = s + bot[t].x;
+        s = s + bot[t].y;
+        float v = s * 0.25f;
+        {
+            const int x = 8 * sx + qx, y = 8 * blockIdx.y + qy;
+            if (x < a.w[3] && y < (a.Hp >> 3)) planes[a.off[3] + (size_t)y * a.w[3] + x] = v;
+        }
+        if constexpr (L >= 4) {
+            v = quad_mean<1, 8>(v);
+            const int x = 4 * sx + (qx >> 1), y = 4 * blockIdx.y + (qy >> 1);
+            if (!(qx & 1) && !(qy & 1) && x < a.w[4] && y < (a.Hp >> 4)) planes[a.off[4] + (size_t)y * a.w[4] + x] = v;
+        }
+        if constexpr (L >= 5) {
+            v = quad_mean<2, 16>(v);
+            const int x = 2 * sx + (qx >> 2), y = 2 * blockIdx.y + (qy >> 2);
+            if (!(qx & 3) && !(qy & 3) && x < a.w[5] && y < (a.Hp >> 5)) planes[a.off[5] + (size_t)y * a.w[5] + x] = v;
+        }
+        if constexpr (L >= 6) {
+            v = quad_mean<4, 32>(v);
+            const int x = sx, y = blockIdx.y;
+            if (lane == 0 && x < a.w[6] && y < (a.Hp >> 6)) planes[a.off[6] + (size_t)y * a.w[6] + x] = v;
+        }
+    }
+}
+
 // Whether the two-kernel pyramid applies: at least levels 1..2 in-kernel and
 // a padded size the level-2 grid and the tail tiles divide.
 bool pyramid2_fits(const PyramidArgs& a)
@@ -369,8 +454,24 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     if (!pyramid2_fits(a) || a.nzero > 64) return hipErrorInvalidValue;
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
-    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (H2 + kPyrRW - 1) / kPyrRW, 2 * batch), dim3(64), 0, s, a);
-    if (a.levels >= 3) {
+    const int nrw = (H2 + kPyrRW - 1) / kPyrRW;  // waves per column
+    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (nrw + kPyrWG - 1) / kPyrWG, 2 * batch), dim3(64 * kPyrWG), 0, s, a);
+#ifndef DIS_TAIL_REG
+#define DIS_TAIL_REG 1
+#endif
+#ifndef DIS_TAIL_REG_TPW
+#define DIS_TAIL_REG_TPW 2
+#endif
+    if (a.levels >= 3 && DIS_TAIL_REG) {
+        constexpr int TPW = DIS_TAIL_REG_TPW;
+        const dim3 grid(((W2 + 15) / 16 + TPW - 1) / TPW, (H2 + 15) / 16, 2 * batch);
+        switch (a.levels) {
+            case 3: hipLaunchKernelGGL((k_pyr_tail_reg<3, TPW>), grid, dim3(64), 0, s, a); break;
+            case 4: hipLaunchKernelGGL((k_pyr_tail_reg<4, TPW>), grid, dim3(64), 0, s, a); break;
+            case 5: hipLaunchKernelGGL((k_pyr_tail_reg<5, TPW>), grid, dim3(64), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_pyr_tail_reg<6, TPW>), grid, dim3(64), 0, s, a); break;
+        }
+    } else if (a.levels >= 3) {
         const int T2 = 1 << (a.levels - 2), TPW = DIS_TAIL_TPW;
         const dim3 grid((W2 / T2 + TPW - 1) / TPW, H2 / T2, 2 * batch);
         switch (a.levels) {

@@ -599,6 +599,13 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
                 b.tile_stride = dis::search8_tile_stride(L.steps, 2);
                 b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, 2) : 0;
             }
+#ifdef DIS_EXP_SKIP_HEAD  // experiment (wrong values): levels >= DIS_EXP_SKIP_HEAD not searched, u = 0
+            if (l >= DIS_EXP_SKIP_HEAD && l > g.F) {
+                DIS_HIP(hipMemset2DAsync(b.u_out, (size_t)g.u_stride * sizeof(float2), 0,
+                                         (size_t)L.n * sizeof(float2), n, s));
+                continue;
+            }
+#endif
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));

@@ -481,6 +481,9 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
 #ifndef DIS_SPLIT_FB
 #define DIS_SPLIT_FB 1
 #endif
+#ifndef DIS_EXP_NO_FB
+#define DIS_EXP_NO_FB 0  // experiment: no k_search8_fb launches (wrong values if a list is not empty)
+#endif
 template <int LPP, bool kFallback>
 constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? DIS_FB_WAVES : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
 
@@ -1150,7 +1153,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     if (L == 1) {
         if (split) {
             DIS_LAUNCH(t, (k_search8<1, false, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
-            hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
+            if (!DIS_EXP_NO_FB) hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<1, true, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
         }
@@ -1160,7 +1163,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
                 launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             else
                 DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
-            hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            if (!DIS_EXP_NO_FB) hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
         }
