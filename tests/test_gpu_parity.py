@@ -43,6 +43,7 @@ CASES = [
     (1000, 200, 4, 1, 8, 6, 0.5, 1),      # pyramid dword row loads (stride, pad_left 4- not 16-byte aligned)
     (432, 320, 4, 1, 8, 6, 0.5, 1),       # pyramid 16-byte row loads, 16 x 16 tiles
     (420, 300, 4, 1, 8, 6, 0.5, 1),       # pad_left 6: byte row loads
+    (800, 600, 5, 2, 8, 8, 0.5, 1),       # C = 5: register pyramid tail, partial 16 x 16 super-tiles
 ]
 
 
