@@ -768,7 +768,11 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     for (size_t i = 0; i < stages.size() * S; ++i) {
         const int k = stage_major ? (int)(i % S) : (int)(i / stages.size());
         const int st = stage_major ? stages[i / S] : stages[i % stages.size()];
+#ifdef DIS_EXP_SPLIT0  // experiment: sub-batch 0 takes n / 2 + DIS_EXP_SPLIT0 pairs (two sub-batches)
+        const int a = k == 0 ? 0 : n / 2 + DIS_EXP_SPLIT0, b = k == 0 ? n / 2 + DIS_EXP_SPLIT0 : n;
+#else
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
+#endif
         hipStream_t sk = k < k0 ? s : c->sub[k];
         StageRange range(st, k);
         dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
