@@ -415,6 +415,12 @@ def main():
                                          "with FMA counted as 2 ops"},
                "stated_tolerance": "DESIGN.md 2 / profiles/tolerance_r02.json; GPU test tests/test_gpu_tolerance.py"}
 
+    # max over ranks of the timed region (before the gather: the timing stands whatever it does)
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
+    if world > 1:
+        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
+    el = float(el_t.item())
+
     # the path's one collective, outside the timed region: the
     # last step's flows of every rank gathered to rank 0 over RCCL/xGMI
     gather = None
@@ -423,13 +429,19 @@ def main():
         barrier()
         torch.cuda.synchronize(dev)
         tg = time.perf_counter()
-        full = multi.gather_flow_tensor(out, world * B, rank, world)
-        torch.cuda.synchronize(dev)
+        try:
+            full = multi.gather_flow_tensor(out, world * B, rank, world)
+            torch.cuda.synchronize(dev)
+            gather_err = None
+        except (RuntimeError, MemoryError) as e:  # reported in the line; the timed result stands
+            full, gather_err = None, f"{type(e).__name__}: {e}"
         tg = time.perf_counter() - tg
         # verify the collective: every rank's bit-level checksum of its own
         # shard against rank 0's checksum of that shard of the gathered tensor
-        sums = multi.gather_checksums(multi.flow_checksum(out), rank, world)
-        if rank == 0:
+        sums = multi.gather_checksums(multi.flow_checksum(out), rank, world) if gather_err is None else None
+        if rank == 0 and gather_err is not None:
+            gather = {"error": gather_err, "world_size": world}
+        elif rank == 0:
             if int(full.shape[0]) != world * B:
                 raise SystemExit(f"bench: gathered {full.shape[0]} pairs, expected {world * B}")
             got = [multi.flow_checksum(full[r * B:(r + 1) * B]) for r in range(world)]
@@ -442,10 +454,6 @@ def main():
                       "world_size": torch.distributed.get_world_size(),
                       "backend": "nccl (RCCL)" if a.dist_backend == "nccl" else a.dist_backend}
             del full
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
-    el = float(el_t.item())
 
     # parity spot check on rank 0: pair 0 of the last step vs the C oracle
     max_epe = None
