@@ -54,6 +54,12 @@
 #ifndef DIS_SPLIT_FENCE
 #define DIS_SPLIT_FENCE false  // sched fence per tap row: 124 VGPRs, measured -1.2 % (r03 A/B)
 #endif
+#ifndef DIS_TAP_PREFETCH
+#define DIS_TAP_PREFETCH 0  // LPP 2 tile path: next update's taps read during the solve (iterate_split)
+#endif
+#ifndef DIS_TAP_PREFETCH_ROWS
+#define DIS_TAP_PREFETCH_ROWS 3
+#endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
 #endif
@@ -402,7 +408,14 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 // products and sums pair the same operands (IEEE mul and add commute), the
 // solve runs on both lanes from the same (c0, c1). `tap_at(cv)` gets the lane's
 // own ceil coordinate.
-template <bool kFence, bool kPaper, bool kFma, typename TapAt>
+//
+// kPrefetch (the LDS-tile path): the 45 taps of the next update are read from
+// LDS while this update's solve runs, at this update's tap base; the next
+// update re-reads them only if some lane's base moved (ceil(p + 1e-5) changed:
+// after the first few updates in ~8 % of wave-iterations at the finest 1080p
+// level), so the LDS latency no longer stalls the top of every update. The
+// tile is read-only during the loop: same values either way.
+template <bool kFence, bool kPaper, bool kFma, bool kPrefetch = false, typename TapAt>
 __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& lu, const float (&g1)[32],
                                               const float (&g2)[32], int q, float rv, float iv, float btv,
                                               float* puv, TapAt&& tap_at)
@@ -415,6 +428,22 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
     const bool f = (lu.swap != 0) != (q != 0);  // c0 takes the partner's right-hand side
     float r[32];
     const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;  // div_pre
+    constexpr int PR = DIS_TAP_PREFETCH_ROWS;  // tap rows read ahead (the rest stream behind them)
+    float T[kPrefetch ? PR : 1][5];
+    int cvl = 0;  // the lane's coordinate of the base T was read at
+    auto load_taps = [&](int cvv) {
+        if constexpr (kPrefetch) {
+            auto tap = tap_at(cvv);
+#pragma unroll
+            for (int k = 0; k < PR; ++k)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) T[k][c] = tap(k, c);
+        }
+    };
+    if constexpr (kPrefetch) {
+        cvl = (int)ceilf(pv + .00001f);
+        load_taps(cvl);
+    }
     for (int counter = 1;; ++counter) {
         // warp_coefs, one coordinate per lane: a (b) = frac, 1 - a (1 - b)
         const float fl = floorf(pv), fr = pv - fl, om = 1 - fr;
@@ -425,7 +454,23 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         w.w1 = xor1f(s1) * s1;    // a (1 - b)
         w.w2 = xor1f(s2w) * s2w;  // b (1 - a)
         w.w3 = xor1f(fr) * fr;    // a b
-        warp_patch<2, kFence, kFma>(w, a.norm, tap_at(cv), r);
+        if constexpr (kPrefetch) {
+            // a pair whose base moved reads at the new one (exec-masked: no
+            // wave-uniform branch, so the read-ahead rows keep their registers)
+            // (both DPP reads before any branch: a short-circuit || would run
+            // the second pair under a divergent mask and read disabled lanes)
+            const int pcv = xor1i(cv), pcvl = xor1i(cvl);
+            const bool moved = (cv != cvl) | (pcv != pcvl);
+            if (moved) {
+                cvl = cv;
+                load_taps(cvl);
+            }
+            auto tap = tap_at(cvl);
+            warp_patch<2, kFence, kFma>(w, a.norm, [&](int k, int c) { return k < PR ? T[k < PR ? k : 0][c] : tap(k, c); },
+                                        r);
+        } else {
+            warp_patch<2, kFence, kFma>(w, a.norm, tap_at(cv), r);
+        }
         float C[4];
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci) {
@@ -440,6 +485,10 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         float bown = (C[0] + C[2]) + (C[1] + C[3]);  // lane 0: b0, lane 1: b1
         if constexpr (kPaper) bown = bown - btv;
         const float bpart = xor1f(bown);
+        if constexpr (kPrefetch) {  // the next update's taps, in flight during the solve
+            load_taps(cvl);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         float d0, c1;
         {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
             float c0 = f ? bpart : bown;
@@ -816,7 +865,8 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // partner's by one DPP add
                 const int M = q ? TS : 1, K = q ? -(5 + ty0) * TS : -(5 + tx0);
                 const float* tq = tile + 4 * q;
-                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, q ? bt1 : bt0, &uv,
+                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, DIS_TAP_PREFETCH>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
+                                                                             q ? bt1 : bt0, &uv,
                                                    [&](int cv) {
                                                        const int t = __mul24(cv, M) + K;
                                                        // three row groups, each one base register and
