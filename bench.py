@@ -62,6 +62,9 @@ def parse():
                     help="skip the extra DIS_PRECISION_FMA measurement (reported beside, never as, value)")
     ap.add_argument("--warmup-floor", type=float, default=WARMUP_FLOOR_S,
                     help="seconds of untimed steps at least (after the W warmup steps); 0 under a profiler")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: shard plan, gather + checksum verification over gloo with stand-in flows, "
+                         "and the line's schema (value null); use with --dist-backend gloo for N > 1")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per search launch (from tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -180,12 +183,110 @@ def check_world(a, world, rank):
     if a.gpus != world:
         raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE {world}: refusing to report a "
                          f"{world}-rank measurement as {a.gpus} GPUs")
-    if a.dist_backend == "nccl" and world > 1:
+    if a.dry_run and world > 1 and a.dist_backend != "gloo":
+        raise SystemExit("bench: --dry-run runs on the CPU: use --dist-backend gloo")
+    if a.dist_backend == "nccl" and world > 1 and not a.dry_run:
         ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
         lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
         if lws > ndev:
             raise SystemExit(f"bench: {lws} local ranks but {ndev} visible GPU(s) under nccl: ranks would "
                              f"share a GPU (use --dist-backend gloo only to rehearse that)")
+
+
+def gather_and_verify(out, B, rank, world, backend, sync=lambda: None, on_full=None):
+    """The path's one collective (SURVEY.md 8e, config 4 "RCCL gather only"):
+    every rank's (B, H, W, 2) flows gathered to rank 0 in pair order
+    (disflow.multi.gather_flow_tensor; RCCL for nccl, host tensors under gloo),
+    then verified: each rank's bit-level checksum of its own shard against rank
+    0's checksum of that shard of the gathered tensor. A failure on any rank is
+    shared (one all-reduce) before the checksum collective, so every rank skips
+    it together. Returns the line's `gather` object on rank 0."""
+    import disflow.multi as multi
+    tg = time.perf_counter()
+    full = None
+    try:
+        full = multi.gather_flow_tensor(out, world * B, rank, world)
+        sync()
+        gather_err = None
+    except (RuntimeError, MemoryError) as e:  # reported in the line; the timed result stands
+        full, gather_err = None, f"{type(e).__name__}: {e}"
+    tg = time.perf_counter() - tg
+    any_err = multi.any_rank_failed(gather_err is not None, world)
+    if any_err and gather_err is None:
+        gather_err = "another rank's gather failed"
+    sums = multi.gather_checksums(multi.flow_checksum(out), rank, world) if not any_err else None
+    if rank != 0:
+        return None
+    if any_err:
+        return {"error": gather_err, "world_size": world}
+    if int(full.shape[0]) != world * B:
+        raise SystemExit(f"bench: gathered {full.shape[0]} pairs, expected {world * B}")
+    got = [multi.flow_checksum(full[r * B:(r + 1) * B]) for r in range(world)]
+    verified = all(torch.equal(g.cpu(), e.cpu()) for g, e in zip(got, sums))
+    if not verified:
+        raise SystemExit("bench: gathered flows differ from the ranks' own flows")
+    if on_full is not None:
+        on_full(full)
+    nbytes = (world - 1) * out.numel() * out.element_size()  # bytes that crossed xGMI
+    return {"ms": tg * 1e3, "bytes_received": nbytes, "GB_per_s": nbytes / tg / 1e9,
+            "pairs": int(full.shape[0]), "verified": verified, "world_size": world,
+            "backend": "nccl (RCCL)" if backend == "nccl" else backend}
+
+
+DRY_HW = (6, 8)  # --dry-run flow fields: tiny, so an 8-rank gloo rehearsal stays cheap
+
+
+def dry_run(a, rank, world):
+    """--dry-run (CPU, no GPU call): the multi-rank plumbing of the bench line
+    exactly as a real N-rank run takes it -- the rank layout, the per-rank
+    shard of the global batch, the gather + checksum verification of
+    gather_and_verify over the process group (gloo here) -- with a
+    deterministic stand-in for the flows (tiny fields, a function of the
+    global pair index, so rank 0 also checks the pair order) -- and the line's
+    schema with `value` null. DIS_BENCH_DRY_FAIL=check|alloc makes rank 0's
+    receive-buffer check or allocation fail (tests)."""
+    import disflow.multi as multi
+    B = a.batch
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+    fail = os.environ.get("DIS_BENCH_DRY_FAIL")
+    if fail == "check":
+        multi.check_gather_fits = lambda nbytes, free, margin=0.9: (_ for _ in ()).throw(
+            MemoryError("dry-run: injected rank-0 receive-buffer check failure"))
+    elif fail == "alloc" and rank == 0:
+        real_empty = torch.empty
+        torch.empty = lambda *s, **k: (_ for _ in ()).throw(RuntimeError("dry-run: injected allocation failure")) \
+            if len(s) and isinstance(s[0], tuple) and s[0][0] == world else real_empty(*s, **k)
+    h, w = DRY_HW
+    a0, a1 = multi.shard_bounds(world * B, rank, world)
+    ids = torch.arange(a0, a1, dtype=torch.float32).view(-1, 1, 1, 1)
+    grid = torch.arange(h * w * 2, dtype=torch.float32).view(1, h, w, 2)
+    out = ids * 1000.0 + grid  # pair k: k*1000 + position
+    order = {}
+
+    def check_order(full):  # rank 0: pair k of the gathered tensor is global pair k
+        want = torch.arange(world * B, dtype=torch.float32).view(-1, 1, 1, 1) * 1000.0 + grid
+        order["pair_order_ok"] = bool(torch.equal(full, want))
+
+    gather = gather_and_verify(out, B, rank, world, "gloo", on_full=check_order) if world > 1 else None
+    if fail == "alloc" and rank == 0:
+        torch.empty = real_empty
+    if rank == 0:
+        if gather is not None and "error" not in gather:
+            gather.update(order)
+        plan = [list(multi.shard_bounds(world * B, r, world)) for r in range(world)]
+        line = {"metric": METRIC, "value": None, "unit": "frame-pairs/s", "n_gpus": world, "steps": a.steps,
+                "warmup": a.warmup, "dry_run": True,
+                "config": {"workload": f"{a.width}x{a.height} preset={a.preset}, {B} pairs/GPU/step, "
+                                       "inputs+outputs in HBM",
+                           "width": a.width, "height": a.height, "preset": a.preset, "global_batch": world * B,
+                           "parallelism": f"pairs sharded over {world} rank(s), no data-path collective"},
+                "shards": plan, "gather": gather,
+                "note": f"--dry-run: no GPU work; stand-in flows of {h}x{w} per pair through the real gather and "
+                        "checksum verification (gloo); value is not measured"}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def main():
@@ -199,6 +300,8 @@ def main():
     if os.environ.get("DIS_BENCH_PLAN_ONLY"):  # tests: the rank layout, before any GPU call
         print(json.dumps({"rank": rank, "world": world, "gpus": a.gpus, "backend": a.dist_backend}), flush=True)
         return
+    if a.dry_run:
+        return dry_run(a, rank, world)
     W, H, B = a.width, a.height, a.batch
     params = disflow.preset_params(disflow.Preset[a.preset.upper()], W, H)
     cpu = None
@@ -425,35 +528,9 @@ def main():
     # last step's flows of every rank gathered to rank 0 over RCCL/xGMI
     gather = None
     if world > 1:
-        import disflow.multi as multi
         barrier()
         torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        try:
-            full = multi.gather_flow_tensor(out, world * B, rank, world)
-            torch.cuda.synchronize(dev)
-            gather_err = None
-        except (RuntimeError, MemoryError) as e:  # reported in the line; the timed result stands
-            full, gather_err = None, f"{type(e).__name__}: {e}"
-        tg = time.perf_counter() - tg
-        # verify the collective: every rank's bit-level checksum of its own
-        # shard against rank 0's checksum of that shard of the gathered tensor
-        sums = multi.gather_checksums(multi.flow_checksum(out), rank, world) if gather_err is None else None
-        if rank == 0 and gather_err is not None:
-            gather = {"error": gather_err, "world_size": world}
-        elif rank == 0:
-            if int(full.shape[0]) != world * B:
-                raise SystemExit(f"bench: gathered {full.shape[0]} pairs, expected {world * B}")
-            got = [multi.flow_checksum(full[r * B:(r + 1) * B]) for r in range(world)]
-            verified = all(torch.equal(g.cpu(), e.cpu()) for g, e in zip(got, sums))
-            if not verified:
-                raise SystemExit("bench: gathered flows differ from the ranks' own flows")
-            nbytes = (world - 1) * out.numel() * out.element_size()  # bytes that crossed xGMI
-            gather = {"ms": tg * 1e3, "bytes_received": nbytes, "GB_per_s": nbytes / tg / 1e9,
-                      "pairs": int(full.shape[0]), "verified": verified,
-                      "world_size": torch.distributed.get_world_size(),
-                      "backend": "nccl (RCCL)" if a.dist_backend == "nccl" else a.dist_backend}
-            del full
+        gather = gather_and_verify(out, B, rank, world, a.dist_backend, sync=lambda: torch.cuda.synchronize(dev))
 
     # parity spot check on rank 0: pair 0 of the last step vs the C oracle
     max_epe = None

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 5
+#define DIS_ABI_VERSION 6
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -90,6 +90,9 @@ typedef struct dis_workload {
 
 int dis_abi_version(void);
 const char* dis_last_error(void);
+/* "product", or "experiment" for a measurement build with DIS_EXP_* knock-out
+ * switches (wrong values by design; csrc/dis_experiments.h) -- ABI v6 */
+const char* dis_build_kind(void);
 
 /* Fill *out with the preset's knobs for a W x H input (C = auto rule). */
 dis_status dis_preset_params(dis_preset preset, int width, int height, dis_params* out);
@@ -177,7 +180,7 @@ dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
  * every level's launches and the join -- instead of ~25 eager launches; a
  * changed key re-captures (an LRU of four executable graphs per context; an
  * exec is updated only after its previous replay has finished). Kernel timing,
- * debug dumps, variational refinement and linked contexts run eagerly. The
+ * debug dumps and variational refinement run eagerly. The
  * capture is thread-local: if another thread synchronises the device or uses
  * the legacy default stream meanwhile, HIP invalidates it and that call runs
  * eagerly instead. Results do not depend on this setting. */
@@ -186,18 +189,9 @@ dis_status dis_set_graphs(dis_ctx* ctx, int enable);
 typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;
 dis_status dis_set_precision(dis_ctx* ctx, int mode);
 
-/* Two batches in flight (ABI v5; serving, no reference counterpart): link two
- * contexts on one device whose calls the caller issues alternately on two
- * streams. Every call of a linked context then starts its front end (pyramid
- * and coarse levels: latency-bound) only once the peer's latest call has
- * reached its VALU-bound levels (the search of level F+1), so one batch's head
- * runs beside the other's body instead of beside the other's head; each
- * context still orders its own calls on its workspace as usual. Linked calls
- * are enqueued eagerly (no graph replay), which costs more than the gating
- * gains: for throughput, leave two engines unlinked on two dedicated streams
- * (INTEGRATION.md). Results do not depend on it.
- * b == NULL unlinks a (and its peer); linking replaces earlier links of both. */
-dis_status dis_pipeline_link(dis_ctx* a, dis_ctx* b);
+/* ABI v6: dis_pipeline_link (v5) is gone -- its linked calls ran eagerly on
+ * the device's shared sub-batch streams and lost to two unlinked contexts on
+ * two caller streams (DESIGN.md 4 "pipelined"), which needs no API. */
 dis_status dis_stage_size(dis_ctx* ctx, int stage, int level, size_t* count);
 dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* dst, size_t count);
 

@@ -131,6 +131,7 @@ struct PyramidArgs {
     int dword_ok;               // I0/I1, stride, pair_stride and pad_left 4-byte aligned: dword row loads
     int qword_ok;               // ... and 16-byte aligned, pad_left a multiple of 16: 16-byte row loads
     unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call start clocks, else null
+    int vec_st;                 // k_pyr12: level-1 / level-2 rows 16-byte aligned (W_2 % 4 == 0; set by launch_pyramid2)
 };
 
 // Fused densify + upsample + crop (dis_frontback.hip).

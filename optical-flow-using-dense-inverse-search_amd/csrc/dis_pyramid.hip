@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_e
         }
         float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 8 * g;
         float* p2 = planes + a.off[2] + (size_t)y2 * W2 + 4 * g;
-        if (np == 4) {  // 16-byte stores (level-1 rows and the level-2 plane are 16-byte aligned: W % 16 == 0 here)
+        if (np == 4 && a.vec_st) {  // 16-byte stores: level-1 rows and the level-2 plane 16-byte aligned (W_2 % 4 == 0)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1]) =
@@ -455,7 +455,12 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
     const int nrw = (H2 + kPyrRW - 1) / kPyrRW;  // waves per column
-    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (nrw + kPyrWG - 1) / kPyrWG, 2 * batch), dim3(64 * kPyrWG), 0, s, a);
+    PyramidArgs b = a;
+    // level-1 rows start at 2 W_2 y floats, level-2 rows at W_2 y (plane
+    // offsets are multiples of 4: Wp, Hp % 4 == 0): 16-byte stores need W_2 % 4 == 0
+    // (with C = 2 or 3, Wp is only a multiple of 4 or 8)
+    b.vec_st = W2 % 4 == 0;
+    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (nrw + kPyrWG - 1) / kPyrWG, 2 * batch), dim3(64 * kPyrWG), 0, s, b);
 #ifndef DIS_TAIL_REG
 #define DIS_TAIL_REG 1
 #endif

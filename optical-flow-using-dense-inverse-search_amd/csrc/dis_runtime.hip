@@ -180,19 +180,13 @@ struct dis_ctx {
     // that exec's last replay has finished (`last`): the update rewrites the
     // kernel arguments an unstarted node of that replay would still read.
     int graphs = 1;
-    // dis_pipeline_link: the peer context whose calls alternate with ours on
-    // another stream; `body` is recorded by every call of a linked context
-    // just before its level-(F+1) search, and the peer's next call waits for it
-    dis_ctx* peer = nullptr;
-    hipEvent_t body = nullptr;
-    bool body_recorded = false;
     static constexpr int kGraphCache = 4;
     struct MainGraph {
         hipGraphExec_t exec = nullptr;
         hipEvent_t last = nullptr;  // recorded after this exec's latest launch
         bool launched = false;
         unsigned long long used = 0;  // LRU clock
-        int n = -1, nsub = -1, precision = -1, variant = -1, linked = -1;
+        int n = -1, nsub = -1, precision = -1, variant = -1;
         const void *i0 = nullptr, *i1 = nullptr;
         void* flow = nullptr;
         size_t stride = 0, pair_stride = 0;
@@ -419,18 +413,6 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
     return d;
 }
 
-// The first of a call's VALU-bound levels (dis_pipeline_link): the search of
-// level F+1, or F when it is the only level.
-int body_level(const dis::Geometry& g) { return g.C > g.F ? g.F + 1 : g.F; }
-
-// A linked context's call first waits for the peer's latest call to reach its
-// body (on the caller's stream, before anything of this call is enqueued).
-dis_status wait_peer(dis_ctx* c, hipStream_t s)
-{
-    if (c->peer && c->peer->body_recorded) DIS_HIP(hipStreamWaitEvent(s, c->peer->body, 0));
-    return DIS_OK;
-}
-
 // One stage of the path for n pairs already resident in device memory: the
 // front end (pyramid), one level (search, and densify + refinement when on),
 // or the back end (output). run_batches issues the stages stage-major across
@@ -499,8 +481,6 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
-        // dis_pipeline_link (linked calls run eagerly: see run_batches_graph)
-        if (c->peer && sub == 0 && l == body_level(g) && !capturing) DIS_HIP(hipEventRecord(c->body, s));
         dis::SearchArgs a{};
         a.img0 = img0;
         a.img1 = img1;
@@ -799,21 +779,16 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
 dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                              size_t pair_stride, float2* flow, hipStream_t s)
 {
-    if (dis_status w = wait_peer(c, s); w != DIS_OK) return w;
     // eager: graphs off, kernel timing, debug dumps, refinement (its own
-    // per-level graphs), and linked contexts (the body event is recorded in
-    // the middle of the call; HIP rejects an external event-record node
-    // under stream capture)
-    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap || c->peer) {
+    // per-level graphs)
+    if (!c->graphs || c->timing || c->debug || c->p.var_refine_iters > 0 || !c->cap) {
         std::lock_guard<std::mutex> lock(pool_mutex(c->device));  // eager enqueue onto the pooled streams
-        const dis_status r = run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
-        if (r == DIS_OK && c->peer) c->body_recorded = true;
-        return r;
+        return run_batches(c, n, I0, I1, stride, pair_stride, flow, s);
     }
     auto key_is = [&](const dis_ctx::MainGraph& G) {
         return G.exec && G.n == n && G.i0 == I0 && G.i1 == I1 && G.flow == flow && G.stride == stride &&
                G.pair_stride == pair_stride && G.nsub == c->nsub && G.precision == c->precision &&
-               G.variant == c->variant && G.linked == (c->peer ? 1 : 0);
+               G.variant == c->variant;
     };
     dis_ctx::MainGraph* G = nullptr;
     for (auto& e : c->mg)
@@ -860,6 +835,16 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
             if (!G->exec) e2 = hipGraphInstantiate(&G->exec, graph, nullptr, nullptr, 0);
         }
         if (graph) hipGraphDestroy(graph);
+        if (r != DIS_OK) {
+            // a real error inside the captured enqueue (not an invalidated
+            // capture): report it; no eager retry on sub-streams that may still
+            // be in a bad capture state
+            (void)hipGetLastError();
+            if (G->exec) hipGraphExecDestroy(G->exec);
+            G->exec = nullptr;
+            G->n = -1;
+            return r;
+        }
         if (e2 != hipSuccess) {
             // The capture was invalidated (e.g. another thread synchronised the
             // device or used the legacy default stream meanwhile) or failed to
@@ -881,7 +866,6 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         G->nsub = c->nsub;
         G->precision = c->precision;
         G->variant = c->variant;
-        G->linked = c->peer ? 1 : 0;
     }
     G->used = ++c->graph_clock;
     if (c->needs_wait(s)) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
@@ -891,7 +875,6 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     }
     DIS_HIP(hipEventRecord(G->last, s));
     G->launched = true;
-    if (c->peer) c->body_recorded = true;  // the graph's event-record node
     c->last_batch = n;
     DIS_HIP(hipEventRecord(c->done, s));
     c->done_pending = true;
@@ -1015,6 +998,7 @@ dis::DensifyArgs densify_level(const dis::Geometry& g, int l, float2* pu, float2
 extern "C" {
 
 int dis_abi_version(void) { return DIS_ABI_VERSION; }
+const char* dis_build_kind(void) { return DIS_BUILD_KIND; }
 
 const char* dis_last_error(void) { return g_err.c_str(); }
 
@@ -1139,8 +1123,7 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&c->body, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess;
     if (ok) {
         size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
         for (int k = 0; k < dis_ctx::kMaxSub; ++k)
@@ -1179,7 +1162,6 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
         }
         if (c->fork) hipEventDestroy(c->fork);
         if (c->done) hipEventDestroy(c->done);
-        if (c->body) hipEventDestroy(c->body);
         if (c->cap) hipStreamDestroy(c->cap);
         if (c->own) hipStreamDestroy(c->own);
         delete c;
@@ -1193,11 +1175,6 @@ dis_status dis_destroy(dis_ctx* c)
 {
     if (!c) return DIS_OK;
     hipSetDevice(c->device);
-    if (c->peer) {  // the peer's next call must not wait on our (destroyed) event
-        c->peer->peer = nullptr;
-        c->peer->body_recorded = false;
-        c->peer = nullptr;
-    }
     if (c->own) hipStreamSynchronize(c->own);
     if (c->done_pending) hipEventSynchronize(c->done);  // the last call, on whatever stream it ran
     for (int k = 0; k < dis_ctx::kMaxSub; ++k)  // the streams are shared (process pool): wait for this
@@ -1210,7 +1187,6 @@ dis_status dis_destroy(dis_ctx* c)
     }
     if (c->fork) hipEventDestroy(c->fork);
     if (c->done) hipEventDestroy(c->done);
-    if (c->body) hipEventDestroy(c->body);
     for (auto& row : c->vrg)
         for (auto& G : row)
             if (G.exec) hipGraphExecDestroy(G.exec);
@@ -1282,28 +1258,6 @@ dis_status dis_set_graphs(dis_ctx* c, int enable)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
     c->graphs = enable ? 1 : 0;
-    return DIS_OK;
-}
-
-dis_status dis_pipeline_link(dis_ctx* a, dis_ctx* b)
-{
-    if (!a) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (a == b) return fail(DIS_ERR_INVALID_ARGUMENT, "a context cannot be linked to itself");
-    if (b && b->device != a->device) return fail(DIS_ERR_INVALID_ARGUMENT, "linked contexts must share a device");
-    auto unlink = [](dis_ctx* c) {
-        if (c->peer) {
-            c->peer->peer = nullptr;
-            c->peer->body_recorded = false;
-        }
-        c->peer = nullptr;
-        c->body_recorded = false;
-    };
-    unlink(a);
-    if (b) {
-        unlink(b);
-        a->peer = b;
-        b->peer = a;
-    }
     return DIS_OK;
 }
 

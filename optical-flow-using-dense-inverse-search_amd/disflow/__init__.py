@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = (
     "dis_workload_info", "dis_create", "dis_destroy", "dis_calc_u8", "dis_calc_batch_u8",
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
-    "dis_set_concurrency", "dis_set_precision", "dis_set_graphs", "dis_pipeline_link", "dis_flow_color", "dis_flo_info", "dis_read_flo", "dis_write_flo",
+    "dis_set_concurrency", "dis_set_precision", "dis_set_graphs", "dis_flow_color", "dis_flo_info",
+    "dis_read_flo", "dis_write_flo", "dis_build_kind",
 )
 
 
@@ -152,8 +153,8 @@ def lib() -> ctypes.CDLL:
         if L.dis_abi_version() >= 4:  # (older builds load for A/B timing only)
             L.dis_set_precision.argtypes = [V, I]
             L.dis_set_graphs.argtypes = [V, I]
-        if L.dis_abi_version() >= 5:
-            L.dis_pipeline_link.argtypes = [V, V]
+        if L.dis_abi_version() >= 6:
+            L.dis_build_kind.restype = ctypes.c_char_p
         L.dis_stage_size.argtypes = [V, I, I, P(Z)]
         L.dis_debug_dump.argtypes = [V, I, I, I, V, Z]
         L.dis_set_kernel_timing.argtypes = [V, I]
@@ -164,10 +165,16 @@ def lib() -> ctypes.CDLL:
         L.dis_read_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
         L.dis_write_flo.argtypes = [ctypes.c_char_p, V, I, I, I]
         for name in EXPORTED_SYMBOLS:
-            if name not in ("dis_abi_version", "dis_last_error") and hasattr(L, name):
+            if name not in ("dis_abi_version", "dis_last_error", "dis_build_kind") and hasattr(L, name):
                 getattr(L, name).restype = I
         _lib = L
     return _lib
+
+
+def build_kind() -> str:
+    """"product", or "experiment" for a knock-out measurement build (wrong values
+    by design, csrc/dis_experiments.h)."""
+    return lib().dis_build_kind().decode()
 
 
 def _check(st: int) -> None:
@@ -296,13 +303,6 @@ class DenseInverseSearch:
     def set_graphs(self, on: bool = True) -> None:
         """Replay batch calls as captured HIP graphs (default on); results are identical."""
         _check(lib().dis_set_graphs(self._ctx, int(on)))
-
-    def pipeline_link(self, other: "DenseInverseSearch | None") -> None:
-        """Two batches in flight (dis_pipeline_link): with calls issued
-        alternately to this engine and `other` on two streams, each call's
-        front end waits for the peer's latest call to reach its VALU-bound
-        levels. None unlinks. Results are identical."""
-        _check(lib().dis_pipeline_link(self._ctx, other._ctx if other is not None else None))
 
     def set_debug(self, on: bool = True) -> None:
         _check(lib().dis_set_debug(self._ctx, int(on)))

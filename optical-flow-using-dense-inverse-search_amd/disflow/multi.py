@@ -154,9 +154,12 @@ def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
     # Every rank checks rank 0's room first (the verdict is shared through the
     # group, so no rank is left blocked in the gather when rank 0 cannot
     # allocate): device memory under RCCL, host memory under gloo.
+    # The receive buffer is allocated BEFORE the broadcast, so an allocation
+    # that fails although the check passed (fragmentation, a concurrent user;
+    # torch raises OutOfMemoryError, a RuntimeError) is shared too.
     nbytes = world * m * int(np.prod(local.shape[1:])) * local.element_size()
     ok = torch.ones(1, dtype=torch.int32, device=local.device)
-    err = None
+    err, buf = None, None
     if rank == 0:
         try:
             if local.is_cuda:
@@ -164,13 +167,14 @@ def gather_flow_tensor(local, n_total: int, rank: int, world: int, group=None):
             else:
                 free = os.sysconf("SC_AVPHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
             check_gather_fits(nbytes, free)
-        except MemoryError as e:
+            buf = torch.empty((world,) + tuple(send.shape), dtype=send.dtype, device=send.device)
+        except (MemoryError, RuntimeError) as e:
             ok.zero_()
-            err = e
+            err = e if isinstance(e, MemoryError) else MemoryError(f"gather: receive buffer allocation failed: {e}")
+            buf = None
     dist.broadcast(ok, src=0, group=group)
     if not int(ok.item()):
         raise err if err is not None else MemoryError("gather: rank 0 has no room for the receive buffer")
-    buf = torch.empty((world,) + tuple(send.shape), dtype=send.dtype, device=send.device) if rank == 0 else None
     recv = list(buf.unbind(0)) if rank == 0 else None
     dist.gather(send.contiguous(), recv, dst=0, group=group)
     if rank != 0:
@@ -193,6 +197,23 @@ def flow_checksum(flows):
     v = flows.contiguous().view(torch.int32).reshape(-1).to(torch.int64)
     w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 65521 + 1
     return torch.stack([v.sum(), (v * w).sum(), torch.tensor(v.numel(), device=v.device)])
+
+
+def any_rank_failed(failed: bool, world: int, group=None, device=None) -> bool:
+    """Collective OR of a per-rank failure flag (all_reduce MAX): every rank
+    gets the same answer, so all take the same branch before the next
+    collective (a failure seen by one rank must not leave the others
+    blocked in a collective it skips)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return failed
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    f = torch.tensor([1 if failed else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(f.item()))
 
 
 def gather_checksums(local_sum, rank: int, world: int, group=None):

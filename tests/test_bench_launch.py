@@ -56,3 +56,41 @@ def test_single_gpu_default_is_one_rank():
     r = subprocess.run([sys.executable, BENCH], env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert [(d["rank"], d["world"], d["gpus"]) for d in _lines(r.stdout)] == [(0, 1, 1)]
+
+
+def _dry(world, **kw):
+    env = _env(**kw)
+    env.pop("DIS_BENCH_PLAN_ONLY")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--dist-backend", "gloo", "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    return lines[0]
+
+
+def test_dry_run_config4_topology_8_ranks():
+    # BASELINE config 4 (256 x 1080p pairs over 8 ranks) rehearsed
+    # on the CPU: 8 gloo ranks, the 256 -> 32-per-rank shard plan, the bench's
+    # own gather + checksum verification (gather_and_verify) and pair order
+    line = _dry(8)
+    assert line["n_gpus"] == 8 and line["value"] is None and line["dry_run"]
+    assert line["config"]["global_batch"] == 256 and line["config"]["width"] == 1920
+    assert line["shards"] == [[32 * r, 32 * (r + 1)] for r in range(8)]
+    g = line["gather"]
+    assert g["pairs"] == 256 and g["verified"] and g["pair_order_ok"] and g["world_size"] == 8
+    assert g["bytes_received"] == 7 * 32 * 6 * 8 * 2 * 4
+
+
+def test_dry_run_rank0_receive_failures_reach_every_rank():
+    # rank 0 cannot hold the receive buffer (the check, or an allocation that
+    # fails although the check passed): every rank leaves the gather together,
+    # the line reports the error, nobody blocks in a collective
+    for fail, text in (("check", "receive-buffer check failure"), ("alloc", "allocation failed")):
+        g = _dry(8, DIS_BENCH_DRY_FAIL=fail)["gather"]
+        assert "error" in g and text in g["error"], g
+
+
+def test_dry_run_uneven_world():
+    line = _dry(3)
+    assert line["shards"] == [[0, 32], [32, 64], [64, 96]] and line["gather"]["pair_order_ok"]
