@@ -161,8 +161,10 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 / 5 = the
  * patch_size-8 search with 4 / 2 / 8 / 1 lanes per patch on every level (5:
  * where the 16x8-patch block fits, grid step <= 7; else 2), 6 = one wave64
- * per patch (lane = pixel) on every exact non-paper level (else 2). All are
- * bit-identical; the switch exists for parity tests and A/B timing. */
+ * per patch (lane = pixel) on every exact non-paper level (else 2), 7 = auto
+ * with the coarse levels as one launch per level instead of the fused head
+ * (k_search8_head, ABI v6). All are bit-identical; the switch exists for
+ * parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 
 /* Arithmetic of the patch_size-8 search kernels (ABI v4; no reference

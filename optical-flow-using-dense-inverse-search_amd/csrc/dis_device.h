@@ -159,12 +159,25 @@ __device__ __forceinline__ float sqrt_cr(float x)
 // image-scale. a = +-0 keeps q0 (the fma steps would turn -0 into +0);
 // b = 0 gives r = inf and NaN instead of +-inf, which the outlier test
 // resets exactly like the reference's inf.
+#ifndef DIS_DIVPRE_BFI
+#define DIS_DIVPRE_BFI 1
+#endif
 __device__ __forceinline__ float div_pre(float a, float b, float r)
 {
     const float q0 = a * r;
     const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
     const float q2 = __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
+#if DIS_DIVPRE_BFI
+    // the sign of q0 on the magnitude of q2 (one v_bfi_b32 instead of a
+    // compare and a VCC select): for a != 0 and finite b the two signs agree
+    // (sign(a / b) = sign(a * RN(1 / b)), signed zeros of an underflow
+    // included), and for a = +-0 q2 is a zero whose sign the fma steps may
+    // have lost while q0's is right -- the bits of `a == 0 ? q0 : q2` for
+    // every finite b (the divisors here are finite: patch sums, weights)
+    return __int_as_float((__float_as_int(q0) & (int)0x80000000) | (__float_as_int(q2) & 0x7fffffff));
+#else
     return a == 0.0f ? q0 : q2;
+#endif
 }
 
 }  // namespace dis

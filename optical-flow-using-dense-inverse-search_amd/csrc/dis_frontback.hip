@@ -351,7 +351,10 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     __shared__ PyrLds<LEVELS> S;
     constexpr int T0 = 1 << LEVELS;
     const int tid = threadIdx.x;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < a.nzero) a.zero[tid] = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+        if (tid < a.nzero) a.zero[tid] = 0;
+        for (int i = tid; i < a.nzero2; i += blockDim.x) a.zero2[i] = 0;
+    }
     // XCD-aware tile order: the dispatcher deals linear block ids round-robin
     // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
     // and horizontally adjacent tiles share their 128-B rows in one L2.

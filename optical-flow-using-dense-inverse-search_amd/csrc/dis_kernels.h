@@ -128,6 +128,8 @@ struct PyramidArgs {
     int w[kMaxLevels];          // plane width per level
     int* zero;                  // nzero ints set to 0 by workgroup 0 (the searches' fallback counts)
     int nzero;
+    int* zero2;                 // nzero2 more (the fused head's counters, k_search8_head), or none
+    int nzero2;
     int dword_ok;               // I0/I1, stride, pair_stride and pad_left 4-byte aligned: dword row loads
     int qword_ok;               // ... and 16-byte aligned, pad_left a multiple of 16: 16-byte row loads
     unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call start clocks, else null
@@ -172,6 +174,24 @@ int search8_tile_stride(int steps, int lanes_per_patch);
 int search8_tile_quad(int steps, int lanes_per_patch);  // LPP 2: 4 x 4-patch half-waves (Search8Args.quad)
 bool search8_lpp1_fits(int steps);
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
+
+// The coarse head in one launch (dis_search8.hip k_search8_head): levels
+// C .. C - nlev + 1, every one at 8 lanes per patch, workgroups ordered level
+// by level (coarsest first, pairs in order); a block of level i starts once
+// every block of its pair at level i - 1 has finished (per-(level, pair)
+// counters `done`, zeroed before the launch) -- the coarse-to-fine order of
+// src/optical_flow.cpp:67-91 without a kernel boundary between the levels.
+constexpr int kHeadMax = 6;
+struct HeadArgs {
+    Search8Args lv[kHeadMax];  // per head level, coarsest first (lanes_per_patch 8)
+    int nbx[kHeadMax], nby[kHeadMax];  // blocks per pair
+    int start[kHeadMax + 1];   // first workgroup of each level
+    int nlev, batch;
+    int* done;                 // [level][pair] finished blocks
+};
+hipError_t launch_search8_head(const HeadArgs& h, hipStream_t s, Timing t = {});
+// blocks per pair of an 8-lanes-per-patch level (8 x 8 patches per block)
+inline int search8_blocks8(int npw, int nph) { return ((npw + 7) / 8) * ((nph + 7) / 8); }
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 
@@ -179,6 +199,8 @@ hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 // maxbits: 32 * n device uints of scratch.
 hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmotion, uint8_t* bgr,
                              unsigned int* maxbits, hipStream_t s);
+// device workspace words launch_flow_color needs for n fields (zeroed by it)
+size_t flow_color_ws_words(int n);
 
 // Variational refinement of one level's dense flow (dis_varref.hip).
 constexpr int kVarRefPlanes = 8;   // per-pair workspace planes

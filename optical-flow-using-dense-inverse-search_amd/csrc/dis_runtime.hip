@@ -206,6 +206,9 @@ struct dis_ctx {
     // of up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
     int* fb = nullptr;
     size_t fb_list_off[8][dis::kMaxLevels] = {};
+    // fused coarse head (k_search8_head): per sub-batch kHeadMax x max_batch
+    // finished-block counters, zeroed by the pyramid kernel of each call
+    int* head_done = nullptr;
     uint8_t* in0 = nullptr;  // host-mode input staging
     uint8_t* in1 = nullptr;
     float2* out = nullptr;   // host-mode output staging
@@ -261,6 +264,8 @@ void free_ws(dis_ctx* c)
     hipFree(c->dense);
     hipFree(c->fb);
     c->fb = nullptr;
+    hipFree(c->head_done);
+    c->head_done = nullptr;
     hipFree(c->vr_ws);
     c->vr_ws = nullptr;
     hipFree(c->in0);
@@ -413,6 +418,28 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
     return d;
 }
 
+#ifndef DIS_HEAD
+#define DIS_HEAD 1  // the coarse head (levels at 8 lanes per patch) as one launch (k_search8_head)
+#endif
+
+// Lowest level of the fused coarse head for a sub-batch of n pairs, or C + 1
+// when there is none: the run of levels C, C-1, ... that search at 8 lanes per
+// patch (at most kHeadMax, at least two), on the plain fast path (patch size
+// 8, no paper mode, refinement or debug dumps; variant 7 = auto without it).
+int head_lo(const dis_ctx* c, int n)
+{
+    const dis::Geometry& g = c->g;
+    const int none = g.C + 1;
+    if (!DIS_HEAD || g.ps != 8 || c->variant == 1 || c->variant == 6 || c->variant == 7 || c->debug ||
+        c->p.paper_mode || c->p.var_refine_iters > 0 || !c->head_done)
+        return none;
+    int l = g.C;
+    while (l >= g.F && g.C - l + 1 <= dis::kHeadMax &&
+           search8_lanes(c->variant, (long long)g.lv[l].npw * g.lv[l].nph * n, g.lv[l].steps) == 8)
+        --l;
+    return g.C - l >= 2 ? l + 1 : none;
+}
+
 // One stage of the path for n pairs already resident in device memory: the
 // front end (pyramid), one level (search, and densify + refinement when on),
 // or the back end (output). run_batches issues the stages stage-major across
@@ -455,6 +482,10 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
             pa.zero = fb_count;
             pa.nzero = g.C + 1;
+            if (head_lo(c, n) <= g.C) {  // the fused head's counters of this sub-batch
+                pa.zero2 = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
+                pa.nzero2 = (g.C + 1 - head_lo(c, n)) * n;
+            }
             pa.stamp = c->stamp ? c->stamp + (size_t)sub * (1 + 2 * dis::kStampN) : nullptr;
             pa.dword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
                             (n > 1 ? pair_stride : 0) | (size_t)g.pad_left) & 3) == 0;
@@ -478,9 +509,65 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         if (!fast || c->debug)  // the fast search computes its template gradients itself
             for (int l = g.F; l <= g.C; ++l) DIS_HIP(dis::launch_sobel(g, l, img0, gdx, gdy, n, s));
     }
+    // the fast search's arguments for level lq of this sub-batch
+    auto make_s8 = [&](int lq) {
+        const dis::LevelGeom& Lq = g.lv[lq];
+        dis::Search8Args b{};
+        b.img0 = img0;
+        b.img1 = img1;
+        b.u_coarse = (lq < g.C) ? pu + g.lv[lq + 1].u_off : nullptr;
+        b.u_out = pu + Lq.u_off;
+        b.plane_stride = g.plane_stride;
+        b.plane_off = Lq.plane_off;
+        b.u_stride = g.u_stride;
+        b.W = Lq.W;
+        b.H = Lq.H;
+        b.steps = Lq.steps;
+        b.npw = Lq.npw;
+        b.nph = Lq.nph;
+        b.offw = Lq.offw;
+        b.offh = Lq.offh;
+        if (lq < g.C) {
+            b.c_npw = g.lv[lq + 1].npw;
+            b.c_nph = g.lv[lq + 1].nph;
+            b.c_offw = g.lv[lq + 1].offw;
+            b.c_offh = g.lv[lq + 1].offh;
+        }
+        b.tmp_lb = Lq.tmp_lb;
+        b.tmp_ub_w = Lq.tmp_ub_w;
+        b.tmp_ub_h = Lq.tmp_ub_h;
+        b.thr_sq = sqrt_threshold((float)g.ps / 2);
+        b.lanes_per_patch = search8_lanes(c->variant, (long long)Lq.npw * Lq.nph * n, Lq.steps);
+        b.tile_stride = dis::search8_tile_stride(Lq.steps, b.lanes_per_patch);
+        b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(Lq.steps, b.lanes_per_patch) : 0;
+        b.fb_count = fb_count + lq;
+        b.fb_list = c->fb + c->fb_list_off[sub][lq];
+        b.paper = paper ? 1 : 0;
+        b.iters = g.iters;
+        b.norm = g.norm;
+        b.fma = (c->precision == DIS_PRECISION_FMA && !paper) ? 1 : 0;
+        return b;
+    };
+    const int hl = fast ? head_lo(c, n) : g.C + 1;
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
+        if (l >= hl) {  // the fused coarse head: all of it at stage C, nothing at its other levels
+            if (l < g.C) continue;
+            dis::HeadArgs h{};
+            h.nlev = g.C - hl + 1;
+            h.batch = n;
+            h.done = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
+            for (int i = 0; i < h.nlev; ++i) {
+                const dis::LevelGeom& Li = g.lv[g.C - i];
+                h.lv[i] = make_s8(g.C - i);
+                h.nbx[i] = (Li.npw + 7) / 8;
+                h.nby[i] = (Li.nph + 7) / 8;
+                h.start[i + 1] = h.start[i] + h.nbx[i] * h.nby[i] * n;
+            }
+            DIS_HIP(dis::launch_search8_head(h, s, timing(c, 1, hl == g.F ? 2 : -1)));
+            continue;
+        }
         dis::SearchArgs a{};
         a.img0 = img0;
         a.img1 = img1;
@@ -509,37 +596,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         a.norm = g.norm;
         a.paper = paper ? 1 : 0;
         if (fast) {
-            dis::Search8Args b{};
-            b.img0 = img0;
-            b.img1 = img1;
-            b.u_coarse = (l < g.C) ? pu + g.lv[l + 1].u_off : nullptr;
-            b.u_out = pu + L.u_off;
-            b.plane_stride = g.plane_stride;
-            b.plane_off = L.plane_off;
-            b.u_stride = g.u_stride;
-            b.W = L.W;
-            b.H = L.H;
-            b.steps = L.steps;
-            b.npw = L.npw;
-            b.nph = L.nph;
-            b.offw = L.offw;
-            b.offh = L.offh;
-            if (l < g.C) {
-                b.c_npw = g.lv[l + 1].npw;
-                b.c_nph = g.lv[l + 1].nph;
-                b.c_offw = g.lv[l + 1].offw;
-                b.c_offh = g.lv[l + 1].offh;
-            }
-            b.tmp_lb = L.tmp_lb;
-            b.tmp_ub_w = L.tmp_ub_w;
-            b.tmp_ub_h = L.tmp_ub_h;
-            b.thr_sq = sqrt_threshold((float)g.ps / 2);
-            b.lanes_per_patch = search8_lanes(c->variant, (long long)L.npw * L.nph * n, L.steps);
-            b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
-            b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, b.lanes_per_patch) : 0;
-            b.fb_count = fb_count + l;
-            b.fb_list = c->fb + c->fb_list_off[sub][l];
-            b.paper = paper ? 1 : 0;
+            dis::Search8Args b = make_s8(l);
             if (paper && !vr && l < g.C) {
                 // weighted initialisation per patch, into this level's (unused) dense slot
                 const dis::LevelGeom& Lc = g.lv[l + 1];
@@ -571,9 +628,6 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
                 b.dense_coarse = dense + g.lv[l + 1].dense_off;
                 b.dense_stride = g.dense_stride;
             }
-            b.iters = g.iters;
-            b.norm = g.norm;
-            b.fma = (c->precision == DIS_PRECISION_FMA && !paper) ? 1 : 0;
             if (b.lanes_per_patch == 64 && (paper || b.fma)) {  // exact, non-paper only
                 b.lanes_per_patch = 2;
                 b.tile_stride = dis::search8_tile_stride(L.steps, 2);
@@ -1132,7 +1186,8 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
                 off += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8) * B;  // 8x8 blocks (the most)
             }
         ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
-             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess;
+             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess &&
+             hipMalloc(&c->head_done, sizeof(int) * dis_ctx::kMaxSub * dis::kHeadMax * B) == hipSuccess;
     }
 #ifdef DIS_STAMP  // diagnostic builds: per-call clocks of each sub-batch stream (tools/stamp_probe.py)
     if (ok && getenv("DIS_STAMP")) {
@@ -1273,7 +1328,7 @@ dis_status dis_set_precision(dis_ctx* c, int mode)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 6) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..6");
+    if (variant < 0 || variant > 7) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..7");
     c->variant = variant;
     return DIS_OK;
 }
@@ -1524,7 +1579,7 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     const size_t cbytes = (size_t)3 * width * height * n;
     if (where == DIS_MEM_DEVICE) {
         unsigned int* maxbits = nullptr;
-        DIS_HIP(hipMallocAsync(reinterpret_cast<void**>(&maxbits), sizeof(unsigned int) * 32 * n, s));
+        DIS_HIP(hipMallocAsync(reinterpret_cast<void**>(&maxbits), sizeof(unsigned int) * dis::flow_color_ws_words(n), s));
         const hipError_t e = dis::launch_flow_color(flow, n, width, height, maxmotion, bgr, maxbits, s);
         DIS_HIP(hipFreeAsync(maxbits, s));
         DIS_HIP(e);
@@ -1535,7 +1590,7 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     unsigned int* maxbits = nullptr;
     dis_status rc = DIS_OK;
     if (hipMalloc(&dflow, fbytes) != hipSuccess || hipMalloc(&dbgr, cbytes) != hipSuccess ||
-        hipMalloc(&maxbits, sizeof(unsigned int) * 32 * n) != hipSuccess) {
+        hipMalloc(&maxbits, sizeof(unsigned int) * dis::flow_color_ws_words(n)) != hipSuccess) {
         rc = fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
     } else if (hipMemcpyAsync(dflow, flow, fbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
                dis::launch_flow_color(dflow, n, width, height, maxmotion, dbgr, maxbits, s) != hipSuccess ||

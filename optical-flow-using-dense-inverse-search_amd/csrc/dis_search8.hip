@@ -57,8 +57,14 @@
 #ifndef DIS_TAP_PREFETCH
 #define DIS_TAP_PREFETCH 0  // LPP 2 tile path: next update's taps read during the solve (iterate_split)
 #endif
+#ifndef DIS_TAP_PREFETCH_FMA
+#define DIS_TAP_PREFETCH_FMA DIS_TAP_PREFETCH  // the same for the tolerance-mode (kFma) kernels
+#endif
 #ifndef DIS_TAP_PREFETCH_ROWS
 #define DIS_TAP_PREFETCH_ROWS 3
+#endif
+#ifndef DIS_RESET_OUT
+#define DIS_RESET_OUT 1  // iterate_split: the outlier reset applied once, after the loop, on the exiting lanes
 #endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
@@ -424,6 +430,7 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
     float uv = iv;
     const float sv = rv + uv;
     float pv = sv;
+    bool reset = false;  // DIS_RESET_OUT: the exit was an outlier / out-of-bounds reset
     const float ubv = q ? a.tmp_ub_h : a.tmp_ub_w;
     const bool f = (lu.swap != 0) != (q != 0);  // c0 takes the partner's right-hand side
     float r[32];
@@ -508,15 +515,25 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         pv = rv + uv;
         const float ev = sv - pv, e2 = ev * ev;
         const float n2 = e2 + xor1f(e2);  // ex * ex + ey * ey
-        const bool bad_own = n2 > a.thr_sq || n2 != n2 || pv < a.tmp_lb || pv > ubv;
-        // either coordinate out: the pair's OR, on the scalar unit
-        unsigned long long m = __builtin_amdgcn_ballot_w64(bad_own);
+        // either coordinate out: the pair's OR, on the scalar unit (one ballot
+        // per compare: each v_cmp writes its lane mask straight to SGPRs)
+        unsigned long long m = __builtin_amdgcn_ballot_w64(n2 > a.thr_sq) | __builtin_amdgcn_ballot_w64(n2 != n2) |
+                               __builtin_amdgcn_ballot_w64(pv < a.tmp_lb) | __builtin_amdgcn_ballot_w64(pv > ubv);
         m |= ((m >> 1) & 0x5555555555555555ull) | ((m << 1) & 0xAAAAAAAAAAAAAAAAull);
         const bool bad = __builtin_amdgcn_inverse_ballot_w64(m);
+#if DIS_RESET_OUT
+        // the reset (u = the initial u, src/patch.cpp:190) on the exiting lanes
+        // only, after the loop: no select per update
+        if (bad || counter > a.iters) {
+            reset = bad;
+            break;
+        }
+#else
         uv = bad ? iv : uv;
         if (bad || counter > a.iters) break;
+#endif
     }
-    *puv = uv;
+    *puv = reset ? iv : uv;
 }
 
 }  // namespace
@@ -865,7 +882,8 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // partner's by one DPP add
                 const int M = q ? TS : 1, K = q ? -(5 + ty0) * TS : -(5 + tx0);
                 const float* tq = tile + 4 * q;
-                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, DIS_TAP_PREFETCH>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
+                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, (kFma ? DIS_TAP_PREFETCH_FMA : DIS_TAP_PREFETCH) != 0>(
+                                                                             a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
                                                                              q ? bt1 : bt0, &uv,
                                                    [&](int cv) {
                                                        const int t = __mul24(cv, M) + K;
@@ -1093,6 +1111,41 @@ k_search8(Search8Args a)
 #endif
 }
 
+// The coarse head in one launch (HeadArgs, dis_kernels.h): workgroup b runs
+// block (bx, by) of pair `pair` at head level i; level i > 0 first waits
+// until every block of the pair at level i - 1 has published its patch
+// displacements (agent-scope release / acquire: the levels' blocks run on any
+// XCD). Deadlock-free with in-order workgroup dispatch: a block waits only
+// for blocks of lower workgroup ids, which were dispatched before it and
+// never wait on it.
+template <bool kFma, int TSC>
+__global__ void __launch_bounds__(kThreads<8>) __attribute__((amdgpu_waves_per_eu(kWaves<8, true>)))
+k_search8_head(HeadArgs h)
+{
+    __shared__ BlockLds<8> S;
+    const int b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < h.nlev && b >= h.start[i + 1]) ++i;
+    const int per = h.nbx[i] * h.nby[i], local = b - h.start[i];
+    const int pair = local / per, blk = local - pair * per;
+    const int by = blk / h.nbx[i], bx = blk - by * h.nbx[i];
+    if (i > 0) {
+        if (threadIdx.x == 0) {
+            const int* d = h.done + (i - 1) * h.batch + pair;
+            const int need = h.nbx[i - 1] * h.nby[i - 1];
+            while (__hip_atomic_load(d, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    search_block<8, true, false, kFma, false, TSC>(h.lv[i], bx, by, pair, S);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this thread's u stores, before the count
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(h.done + i * h.batch + pair, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
 // (usually empty: every workgroup reads the count and exits).
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
@@ -1241,6 +1294,33 @@ static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 gr
     } else {
         hipLaunchKernelGGL((k_search8<8, true, false, false, true>), grid, dim3(kThreads<8>), 0, s, a);
     }
+}
+
+hipError_t launch_search8_head(const HeadArgs& h, hipStream_t s, Timing t)
+{
+    if (h.nlev < 1 || h.nlev > kHeadMax || !h.done || h.batch < 1) return hipErrorInvalidValue;
+    for (int i = 0; i < h.nlev; ++i) {
+        const Search8Args& a = h.lv[i];
+        if (a.lanes_per_patch != 8 || a.paper || a.gdx_plane || a.dense_coarse || a.u_init ||
+            a.tile_stride != h.lv[0].tile_stride || a.tile_stride < kTileW<2> + 1 || a.tile_stride > kTSMax<2> ||
+            (7 * a.steps + 11) * (7 * a.steps + 10) > kTileH * kTSMax<2> ||
+            h.nbx[i] != (a.npw + kBX<8> - 1) / kBX<8> || h.nby[i] != (a.nph + kBY - 1) / kBY ||
+            h.start[i + 1] - h.start[i] != h.nbx[i] * h.nby[i] * h.batch || (i > 0 && !a.u_coarse))
+            return hipErrorInvalidValue;
+    }
+    if (h.start[0] != 0) return hipErrorInvalidValue;
+    const dim3 grid(h.start[h.nlev]), block(kThreads<8>);
+#define DIS_HEAD_LAUNCH(FMA, TS) DIS_LAUNCH(t, (k_search8_head<FMA, TS>), grid, block, 0, s, h)
+    const bool fma = h.lv[0].fma != 0;
+    switch (DIS_STATIC_TS ? h.lv[0].tile_stride : 0) {
+        case 65: if (fma) DIS_HEAD_LAUNCH(true, 65); else DIS_HEAD_LAUNCH(false, 65); break;
+        case 66: if (fma) DIS_HEAD_LAUNCH(true, 66); else DIS_HEAD_LAUNCH(false, 66); break;
+        case 68: if (fma) DIS_HEAD_LAUNCH(true, 68); else DIS_HEAD_LAUNCH(false, 68); break;
+        case 72: if (fma) DIS_HEAD_LAUNCH(true, 72); else DIS_HEAD_LAUNCH(false, 72); break;
+        default: if (fma) DIS_HEAD_LAUNCH(true, 0); else DIS_HEAD_LAUNCH(false, 0); break;
+    }
+#undef DIS_HEAD_LAUNCH
+    return hipGetLastError();
 }
 
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t)

@@ -288,7 +288,9 @@ class DenseInverseSearch:
                                        MEM_DEVICE, stream or None))
 
     def set_variant(self, variant: int) -> None:
-        """0 = specialised kernels (2 lanes/patch search), 1 = generic only, 2 = 4 lanes/patch."""
+        """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels,
+        fused coarse head), 1 = generic only, 2 / 3 / 4 / 5 = 4 / 2 / 8 / 1 lanes per
+        patch, 6 = one wave per patch, 7 = auto with one launch per coarse level."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
 
     def set_concurrency(self, streams: int) -> None:

@@ -461,10 +461,44 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
     exp = oracle.calc_from_params(I0, I1, p)
     exp_fb = oracle.calc_from_params(J0, J1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64")):
+    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64"),
+                          (7, "auto, no fused head")):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
+
+
+HEAD_CASES = [
+    # (W, H, preset, batch, streams, variant, fma): the fused coarse head
+    # (k_search8_head) against the per-level launches (variant 7) and the oracle
+    (1920, 1080, "MEDIUM", 3, 1, 0, 0),   # levels 6..4 in one launch (3 pairs)
+    (1920, 1080, "MEDIUM", 4, 2, 0, 1),   # two sub-batches, tolerance mode (vs variant 7 only)
+    (640, 480, "ULTRAFAST", 5, 2, 0, 0),  # C 4 .. (levels at 8 lanes per patch)
+    (320, 240, "MEDIUM", 2, 1, 4, 0),     # every level at 8 lanes: the head reaches the finest level
+    (203, 151, "SLOW", 3, 3, 4, 0),       # ragged, F = 0, three sub-batches of one pair
+]
+
+
+@pytest.mark.parametrize("W,H,preset,B,streams,variant,fma", HEAD_CASES)
+def test_fused_head_bitexact(disflow_mod, oracle, W, H, preset, B, streams, variant, fma):
+    p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
+    if preset == "SLOW":
+        p.iterations = 16
+    pairs = [disflow_mod.synth_pair(900 + 7 * k + W, W, H) for k in range(B)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=B)
+    eng.set_concurrency(streams)
+    eng.set_precision(fma)
+    eng.set_variant(variant)
+    got = eng.calc_batch(I0, I1)
+    eng.set_variant(7 if variant == 0 else 3)  # per-level launches (variant 3: 2 lanes everywhere)
+    ref = eng.calc_batch(I0, I1)
+    if variant == 0:
+        _assert_bitexact(got, ref, "fused head vs per-level launches")
+    if not fma:
+        for k in range(B):
+            _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"pair {k} vs oracle")
 
 
 @pytest.mark.gpu
@@ -524,6 +558,37 @@ def test_flow_color_kernel_bitexact(disflow_mod, oracle, maxmotion):
     for k in range(3):
         assert np.array_equal(got[k], oracle.flow_color(f[k], maxmotion)), f"field {k}"
     assert np.array_equal(disflow_mod.flow_color(flow, maxmotion), oracle.flow_color(flow, maxmotion))
+
+
+@pytest.mark.parametrize("maxmotion", [-1.0, 2.5, 1e-30, 1e30])
+def test_flow_color_batch_persistent_bitexact(disflow_mod, oracle, maxmotion):
+    # the one-launch colour kernel (k_color: max-pass and colour work items
+    # claimed in order, colour items of field f waiting for f's max): a batch
+    # of 5 fields (W*H % 4 == 0: float4 loads, dwordx3 stores), ragged values
+    # per field, and maxmotion outside div_pre's domain (IEEE division path)
+    rng = np.random.default_rng(11)
+    f = (rng.standard_normal((5, 96, 128, 2)) * np.array([0.5, 3, 20, 1e-3, 60])[:, None, None, None]).astype(np.float32)
+    f[1, 3, :4] = [(np.nan, 0), (1e9, 1), (-0.0, -0.0), (1e-40, 3e-39)]
+    f[4, :, :] = 0.0  # a field with maxrad 0 -> max(1, 0)
+    got = disflow_mod.flow_color(f, maxmotion)
+    for k in range(5):
+        assert np.array_equal(got[k], oracle.flow_color(f[k], maxmotion)), f"field {k}"
+
+
+def test_flow_color_unaligned_output_bitexact(disflow_mod, oracle):
+    # a BGR pointer that is not 4-byte aligned takes the per-pixel store path
+    import torch
+    rng = np.random.default_rng(12)
+    f = (rng.standard_normal((3, 40, 64, 2)) * 4).astype(np.float32)
+    d = torch.from_numpy(f).cuda()
+    raw = torch.zeros(3 * 40 * 64 * 3 + 1, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    disflow_mod._check(disflow_mod.lib().dis_flow_color(d.data_ptr(), 3, 64, 40, -1.0, raw.data_ptr() + 1,
+                                                        disflow_mod.MEM_DEVICE, s.cuda_stream, 0))
+    s.synchronize()
+    o = raw.cpu().numpy()[1:].reshape(3, 40, 64, 3)
+    for k in range(3):
+        assert np.array_equal(o[k], oracle.flow_color(f[k]))
 
 
 def test_flow_color_device_pointers(disflow_mod, oracle):

@@ -109,9 +109,14 @@ def run_colour(steps, warmup):
         call()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
-    moved = B * W * H * (8 * 2 + 3)  # flow read twice (max radius, colour), BGR written
+    # algorithmic bytes per field: the flow read once (8 B/px) and the BGR image
+    # written (3 B/px); the max-radius pass's second read of each field is
+    # served from the L2 / MALL in k_color (dis_color.hip), so it is not counted
+    per_field = W * H * (8 + 3)
+    moved = B * per_field
     return {"config": "colour 1920x1080 x32", "ms_per_call": el * 1e3, "fields_per_s": B / el,
-            "hbm_gbs": moved / el / 1e9, "hbm_frac": moved / el / 8e12}
+            "algorithmic_bytes_per_field": per_field, "hbm_gbs": moved / el / 1e9, "hbm_frac": moved / el / 8e12,
+            "hbm_frac_two_reads": B * W * H * (8 * 2 + 3) / el / 8e12}
 
 
 def run_compat(steps, warmup):

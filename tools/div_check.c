@@ -1,7 +1,8 @@
 /* div_check -- CPU check of the search loop's division by a pre-computed
  * reciprocal (dis_search8.hip div_pre) against IEEE single division:
  * q0 = a*r, q1 = fma(fma(-b,q0,a),r,q0), q2 = fma(fma(-b,q1,a),r,q1),
- * r = RN(1/b); a = +-0 keeps q0. Random a, b with exponents in [-60, 60]
+ * r = RN(1/b), then q0's sign bit on q2's magnitude (the kernels' form since
+ * r04; the same bits as "a = +-0 keeps q0"). Random a, b with exponents in [-60, 60]
  * (the patch sums and LU pivots of 8-bit images) and mantissas biased to the
  * edge cases (all ones, zero). Usage: div_check [samples]; exit 1 on a
  * mismatch. A second pass checks the output kernel's densify divisors
@@ -23,7 +24,7 @@ static float div_pre(float a, float b, float r)
     const float q0 = a * r;
     const float q1 = fmaf(fmaf(-b, q0, a), r, q0);
     const float q2 = fmaf(fmaf(-b, q1, a), r, q1);
-    return a == 0.0f ? q0 : q2;
+    return bf((fb(q0) & 0x80000000u) | (fb(q2) & 0x7fffffffu));
 }
 
 int main(int argc, char** argv)

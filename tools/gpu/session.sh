@@ -9,6 +9,9 @@
 #   levels=<lib>,<lib>,...       per-kernel one-stream durations (rocprof kernel trace)
 #   pmc=<lib>                    SQ counters of the top kernels (tools/gpu/pmc_sq.sh; CTRS= to override)
 #   bench                        bench.py default line
+#   smoke                        __graft_entry__.smoke()
+#   tool=<name> [args]           a built tools/ binary (e.g. tool=issue_mix)
+#   py=<script> [args]           a python script of the repo (e.g. py="tools/bench_configs.py --configs colour")
 # Libraries are paths relative to the package's disflow/ (e.g. libdis_hip_x.so);
 # build variants first on the CPU: tools/build_variants.sh name:"-DFLAG=1".
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
@@ -32,6 +35,9 @@ for s in "$@"; do
     levels) run s${n}_levels 600 bash tools/gpu/levels.sh $(libs "$v") ;;
     pmc) run s${n}_pmc 300 bash tools/gpu/pmc_sq.sh $(libs "$v") ;;
     bench) run s${n}_bench 400 python bench.py ;;
+    smoke) run s${n}_smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tool) run s${n}_$(echo "$v" | cut -d' ' -f1) 300 ./tools/$v ;;
+    py) run s${n}_$(basename "$(echo "$v" | cut -d' ' -f1)" .py) 600 python3 $v ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
