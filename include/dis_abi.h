@@ -162,9 +162,11 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * patch_size-8 search with 4 / 2 / 8 / 1 lanes per patch on every level (5:
  * where the 16x8-patch block fits, grid step <= 7; else 2), 6 = one wave64
  * per patch (lane = pixel) on every exact non-paper level (else 2), 7 = auto
- * with the coarse levels as one launch per level instead of the fused head
- * (k_search8_head, ABI v6). All are bit-identical; the switch exists for
- * parity tests and A/B timing. */
+ * with one launch per coarse level (what 0 does in the default build), 8 =
+ * auto with the coarse levels at 8 lanes per patch fused into one launch
+ * (k_search8_head, ABI v6; measured 0.6-1.0 % slower per step, so not the
+ * default). All are bit-identical; the switch exists for parity tests and A/B
+ * timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 
 /* Arithmetic of the patch_size-8 search kernels (ABI v4; no reference

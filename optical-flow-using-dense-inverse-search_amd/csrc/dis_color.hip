@@ -1,7 +1,7 @@
 // dis_color.hip -- Middlebury flow colour coding:
 // draw_optical_flow / compute_color, src/color_coding.cpp:13-117.
 //
-// One persistent kernel over a batch of n W x H (u,v) fields (k_color, below):
+// Two kernels over a batch of n W x H (u,v) fields (k_color_max, k_color_px):
 // per field the motion range (maxrad = max(1, max |u| over valid pixels),
 // :88-104) and then every pixel to BGR u8 (:106-115; invalid pixels stay
 // black). The float expressions are the reference's, in its order,
@@ -77,12 +77,10 @@ __device__ __forceinline__ bool flow_ok(float x, float y)
     return !(x != x) && !(y != y) && fabsf(x) < 1e9f && fabsf(y) < 1e9f;
 }
 
-constexpr int kMaxStride = 32;  // per field: [0] max radius bits, [1] finished max-pass items (one 128-B line)
+constexpr int kMaxStride = 32;  // per field: [0] max radius bits (one 128-B line per field)
 constexpr int kThreads = 256;
-constexpr int kApx = kThreads * 64;  // pixels per max-pass item (each lane: 32 float4 = 64 vectors)
 constexpr int kBG = 4;               // colour item: kBG groups of 4 consecutive pixels per lane
 constexpr int kBpx = kThreads * 4 * kBG;  // pixels per colour item
-constexpr int kClaim = 8;            // consecutive items per ticket (one atomic per kClaim items)
 
 // u / m correctly rounded for a per-field divisor m given rm = RN(1/m)
 // (div_pre, dis_device.h), on the domain where its remainders cannot
@@ -97,20 +95,26 @@ __device__ __forceinline__ float div_field(float u, float m, float rm, bool fast
 // with compute_color (:13-79) -> packed B | G << 8 | R << 16 (0 when invalid:
 // dst.setTo(0), :87). `col` = the wheel as floats (c_wheel / 255.f, the same
 // IEEE quotients the reference forms per pixel).
-__device__ __forceinline__ unsigned color_px(float2 u, float maxrad, float rmax, bool fast, const float (*col)[3])
+__device__ __forceinline__ unsigned color_px(float2 u, float maxrad, float rmax, bool fast, const float4* col)
 {
     if (!flow_ok(u.x, u.y)) return 0u;
     const float fx = div_field(u.x, maxrad, rmax, fast), fy = div_field(u.y, maxrad, rmax, fast);  // (:113)
     const float rad = sqrtf(fx * fx + fy * fy);
-    const float a = atan2_dis(-fy, -fx) / 3.14159274f;  // (float)CV_PI
+    // atan2(...) / (float)CV_PI, correctly rounded through RN(1 / pi) (div_pre)
+    // on its domain, the IEEE division for |t| < 2^-60
+    constexpr float kPi = 3.14159274f, kRPi = 1.0f / kPi;
+    const float t = atan2_dis(-fy, -fx);
+    const float a = div_field(t, kPi, kRPi, true);
     const float fk = (a + 1.0f) / 2.0f * (float)(kNCols - 1);
     const int k0 = (int)fk;
     const int k1 = k0 + 1 == kNCols ? 0 : k0 + 1;  // (k0 + 1) % ncols, k0 in [0, ncols - 1]
     const float f = fk - (float)k0;
     unsigned o = 0;
+    const float4 w0 = col[k0], w1 = col[k1];  // (r, g, b) of the two wheel entries
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
-        float c = (1 - f) * col[k0][b] + f * col[k1][b];
+        const float c0 = b == 0 ? w0.x : b == 1 ? w0.y : w0.z, c1 = b == 0 ? w1.x : b == 1 ? w1.y : w1.z;
+        float c = (1 - f) * c0 + f * c1;
         if (rad <= 1)
             c = 1 - rad * (1 - c);  // increase saturation with radius
         else
@@ -120,145 +124,95 @@ __device__ __forceinline__ unsigned color_px(float2 u, float maxrad, float rmax,
     return o;
 }
 
-// One persistent launch over a work list of max-pass items A(f) (per field,
-// kApx pixels each: the valid-pixel max radius, :88-104, reduced per
-// workgroup into one float-bit atomicMax -- a max is order-independent, so the
-// result is exact) and colour items B(f) (kBpx pixels each), claimed in order,
-// kClaim consecutive items per atomic ticket (one ticket per item was
-// measured 10x slower: 97k atomics on one address serialise): A(0), A(1),
-// B(0), A(2), B(1), ..., B(n-1). B(f) waits until every A(f) item has
-// finished; all of them were claimed before it by running workgroups, which
-// work through their claims in order and wait only for lower items, so the
-// lowest unfinished item can always proceed. Field
-// f's flow is re-read by B(f) one field after A(f) read it, from the L2 / MALL
-// (16.6 MB per 1080p field) rather than HBM: the flow crosses HBM about once.
-// With maxmotion > 0 there are no A items and no waits. Each colour lane reads
-// its 4 pixels as two float4 and writes 12 bytes with one dwordx3 store when
-// the field size and pointers allow (vec), else per pixel.
+// Two kernels per chunk of fields, the chunk sized so that its flow stays in
+// the 256 MiB Infinity Cache between them (a chunk's fields ~128 MB): the max
+// pass reads the flow from HBM, the colour pass re-reads it from the cache, so
+// the flow crosses HBM about once. (A single persistent launch with a work
+// queue -- max-pass and colour items claimed through an atomic ticket, colour
+// items of field f waiting for f's max -- measured 2.1 ms per 32 1080p fields
+// against 0.51 ms for the r03 two-kernel form: not kept.)
 struct ColorArgs {
-    const float2* flow;
-    uint8_t* bgr;
-    unsigned int* ws;  // kMaxStride per field (zeroed), then the ticket at [kMaxStride * n]
+    const float2* flow;  // the chunk's first field
+    uint8_t* bgr;        // its first image
+    unsigned int* ws;    // kMaxStride per field of the chunk: [0] max radius bits
     long long npix;
-    int n, na, nb;     // fields, A / B items per field (na = 0: fixed maxmotion)
-    float maxmotion;
-    int vec;
+    float maxmotion;     // > 0: fixed range (ws unused)
+    int vec;             // float4 loads / dwordx3 stores (npix % 4 == 0, aligned pointers)
 };
 
-// work item t -> (max pass?, field, chunk) in the order A(0) | A(f+1), B(f) ... | B(n-1)
-__device__ __forceinline__ void color_item(const ColorArgs& a, long long t, bool& isA, int& f, int& chunk)
+// grid (blocks, fields): the valid-pixel max radius of each field (:88-104),
+// reduced per workgroup into one float-bit atomicMax (a max is
+// order-independent: exact)
+__global__ void __launch_bounds__(kThreads) k_color_max(ColorArgs a)
 {
-    if (a.na == 0) {
-        isA = false, f = (int)(t / a.nb), chunk = (int)(t % a.nb);
-    } else if (t < a.na) {
-        isA = true, f = 0, chunk = (int)t;
-    } else {
-        const long long r = t - a.na, per = a.na + a.nb;
-        const int g = (int)(r / per), o = (int)(r % per);  // group g: A(g + 1) then B(g)
-        if (g < a.n - 1) {
-            isA = o < a.na, f = isA ? g + 1 : g, chunk = isA ? o : o - a.na;
+    __shared__ float red[kThreads / 64];
+    const int f = blockIdx.y;
+    const float2* fl = a.flow + (size_t)f * a.npix;
+    float m = 0.0f;
+    const long long step = 2LL * kThreads * gridDim.x;
+    for (long long i = 2LL * ((long long)blockIdx.x * kThreads + threadIdx.x); i < a.npix; i += step) {
+        if (a.vec && i + 2 <= a.npix) {
+            const float4 u = *reinterpret_cast<const float4*>(fl + i);
+            if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));  // (:101)
+            if (flow_ok(u.z, u.w)) m = fmaxf(m, sqrtf(u.z * u.z + u.w * u.w));
         } else {
-            isA = false, f = a.n - 1, chunk = (int)(r - (long long)(a.n - 1) * per);
+            for (long long q = i; q < i + 2 && q < a.npix; ++q) {
+                const float2 u = fl[q];
+                if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));
+            }
         }
     }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        atomicMax(&a.ws[(size_t)kMaxStride * f], __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
-__global__ void __launch_bounds__(kThreads) k_color(ColorArgs a)
+// grid (ceil(npix / kBpx), fields): each lane colours kBG groups of 4
+// consecutive pixels, all its loads in flight before any is consumed
+__global__ void __launch_bounds__(kThreads) k_color_px(ColorArgs a)
 {
-    __shared__ float col[kNCols][3];
-    __shared__ float red[kThreads / 64];
-    __shared__ long long claim;
-    for (int i = threadIdx.x; i < kNCols * 3; i += kThreads) col[i / 3][i % 3] = (float)c_wheel.rgb[i / 3][i % 3] / 255.f;
-    const long long total = (long long)(a.na + a.nb) * a.n;
-    unsigned int* const ticket = a.ws + (size_t)kMaxStride * a.n;
-    for (;;) {
-        __syncthreads();  // the previous claim's LDS use is over (and col is staged)
-        // kClaim consecutive items per ticket, processed in order: every item
-        // is owned by a running workgroup from the moment it is claimed
-        if (threadIdx.x == 0) claim = (long long)atomicAdd(ticket, 1u) * kClaim;
-        __syncthreads();
-        const long long t0 = claim;
-        if (t0 >= total) return;
-        for (long long t = t0; t < t0 + kClaim && t < total; ++t) {
-            int f, chunk;
-            bool isA;
-            color_item(a, t, isA, f, chunk);
-            const float2* fl = a.flow + (size_t)f * a.npix;
-            unsigned int* const fw = a.ws + (size_t)kMaxStride * f;
-            if (isA) {
-                float m = 0.0f;
-                const long long p0 = (long long)chunk * kApx;
-#pragma unroll 8
-                for (int k = 0; k < kApx / (2 * kThreads); ++k) {
-                    const long long i = p0 + 2 * (k * kThreads + threadIdx.x);  // 2 pixels per lane and step
-                    if (a.vec && i + 2 <= a.npix) {
-                        const float4 u = *reinterpret_cast<const float4*>(fl + i);
-                        if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));  // (:101)
-                        if (flow_ok(u.z, u.w)) m = fmaxf(m, sqrtf(u.z * u.z + u.w * u.w));
-                    } else {
-                        for (long long q = i; q < i + 2 && q < a.npix; ++q) {
-                            const float2 u = fl[q];
-                            if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));
-                        }
-                    }
-                }
-                for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-                __syncthreads();  // red[] of the previous item read
-                if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-                    atomicMax(&fw[0], __float_as_uint(m));
-                    __hip_atomic_fetch_add(&fw[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                continue;
-            }
-            // maxrad = maxmotion, or max(1, max radius) when maxmotion <= 0 (:88-104)
-            float maxrad = a.maxmotion;
-            if (a.na) {
-                __syncthreads();  // red[] of the previous item read
-                if (threadIdx.x == 0) {
-                    while (__hip_atomic_load(&fw[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)a.na)
-                        __builtin_amdgcn_s_sleep(2);
-                    red[0] = fmaxf(1.0f, __uint_as_float(__hip_atomic_load(&fw[0], __ATOMIC_RELAXED,
-                                                                           __HIP_MEMORY_SCOPE_AGENT)));
-                }
-                __syncthreads();
-                maxrad = red[0];
-            }
-            const bool fast = maxrad >= 0x1p-60f && maxrad <= 0x1p60f;
-            const float rmax = 1.0f / maxrad;
-            const long long pb = (long long)chunk * kBpx + 4 * threadIdx.x;
-            if (a.vec && pb + 4 * kThreads * (kBG - 1) + 4 <= a.npix) {
-                float4 v[kBG][2];  // all the lane's loads in flight before any is consumed
+    __shared__ float4 col[kNCols];  // the wheel as floats, one 16-byte entry per colour
+    for (int i = threadIdx.x; i < kNCols; i += kThreads)
+        col[i] = make_float4((float)c_wheel.rgb[i][0] / 255.f, (float)c_wheel.rgb[i][1] / 255.f,
+                             (float)c_wheel.rgb[i][2] / 255.f, 0.0f);
+    __syncthreads();
+    const int f = blockIdx.y;
+    const float2* fl = a.flow + (size_t)f * a.npix;
+    // maxrad = maxmotion, or max(1, max radius) when maxmotion <= 0 (:88-104)
+    const float maxrad = a.maxmotion > 0.0f ? a.maxmotion : fmaxf(1.0f, __uint_as_float(a.ws[(size_t)kMaxStride * f]));
+    const bool fast = maxrad >= 0x1p-60f && maxrad <= 0x1p60f;
+    const float rmax = 1.0f / maxrad;
+    const long long pb = (long long)blockIdx.x * kBpx + 4 * threadIdx.x;
+    uint8_t* const out = a.bgr + (size_t)f * a.npix * 3;
+    if (a.vec && pb + 4 * kThreads * (kBG - 1) + 4 <= a.npix) {
+        float4 v[kBG][2];
 #pragma unroll
-                for (int g = 0; g < kBG; ++g) {
-                    const long long p0 = pb + 4 * kThreads * g;
-                    v[g][0] = *reinterpret_cast<const float4*>(fl + p0);
-                    v[g][1] = *reinterpret_cast<const float4*>(fl + p0 + 2);
-                }
+        for (int g = 0; g < kBG; ++g) {
+            const long long p0 = pb + 4 * kThreads * g;
+            v[g][0] = *reinterpret_cast<const float4*>(fl + p0);
+            v[g][1] = *reinterpret_cast<const float4*>(fl + p0 + 2);
+        }
 #pragma unroll
-                for (int g = 0; g < kBG; ++g) {
-                    const long long p0 = pb + 4 * kThreads * g;
-                    const unsigned c0 = color_px(make_float2(v[g][0].x, v[g][0].y), maxrad, rmax, fast, col);
-                    const unsigned c1 = color_px(make_float2(v[g][0].z, v[g][0].w), maxrad, rmax, fast, col);
-                    const unsigned c2 = color_px(make_float2(v[g][1].x, v[g][1].y), maxrad, rmax, fast, col);
-                    const unsigned c3 = color_px(make_float2(v[g][1].z, v[g][1].w), maxrad, rmax, fast, col);
-                    // 4 pixels x 3 bytes, little-endian: c0 | c1 << 24, c1 >> 8 | c2 << 16, c2 >> 16 | c3 << 8
-                    *reinterpret_cast<uint3*>(a.bgr + ((size_t)f * a.npix + p0) * 3) =
-                        make_uint3(c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8));
-                }
-            } else {
-                for (int g = 0; g < kBG; ++g) {
-                    const long long p0 = pb + 4 * kThreads * g;
-                    for (long long q = p0; q < p0 + 4 && q < a.npix; ++q) {
-                        const unsigned c = color_px(fl[q], maxrad, rmax, fast, col);
-                        uint8_t* px = a.bgr + ((size_t)f * a.npix + q) * 3;
-                        px[0] = (uint8_t)c;
-                        px[1] = (uint8_t)(c >> 8);
-                        px[2] = (uint8_t)(c >> 16);
-                    }
-                }
+        for (int g = 0; g < kBG; ++g) {
+            const long long p0 = pb + 4 * kThreads * g;
+            const unsigned c0 = color_px(make_float2(v[g][0].x, v[g][0].y), maxrad, rmax, fast, col);
+            const unsigned c1 = color_px(make_float2(v[g][0].z, v[g][0].w), maxrad, rmax, fast, col);
+            const unsigned c2 = color_px(make_float2(v[g][1].x, v[g][1].y), maxrad, rmax, fast, col);
+            const unsigned c3 = color_px(make_float2(v[g][1].z, v[g][1].w), maxrad, rmax, fast, col);
+            // 4 pixels x 3 bytes, little-endian: c0 | c1 << 24, c1 >> 8 | c2 << 16, c2 >> 16 | c3 << 8
+            *reinterpret_cast<uint3*>(out + p0 * 3) =
+                make_uint3(c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8));
+        }
+    } else {
+        for (int g = 0; g < kBG; ++g) {
+            const long long p0 = pb + 4 * kThreads * g;
+            for (long long q = p0; q < p0 + 4 && q < a.npix; ++q) {
+                const unsigned c = color_px(fl[q], maxrad, rmax, fast, col);
+                out[q * 3] = (uint8_t)c;
+                out[q * 3 + 1] = (uint8_t)(c >> 8);
+                out[q * 3 + 2] = (uint8_t)(c >> 16);
             }
         }
     }
@@ -270,25 +224,34 @@ hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmo
                              unsigned int* ws, hipStream_t s)
 {
     ColorArgs a{};
-    a.flow = reinterpret_cast<const float2*>(flow);
-    a.bgr = bgr;
-    a.ws = ws;
     a.npix = (long long)W * H;
-    a.n = n;
-    a.na = maxmotion > 0.0f ? 0 : (int)((a.npix + kApx - 1) / kApx);
-    a.nb = (int)((a.npix + kBpx - 1) / kBpx);
     a.maxmotion = maxmotion;
-    // dwordx3 stores of 4 pixels at byte 12 k of a field, float4 loads of 2 pixels
     a.vec = a.npix % 4 == 0 && (reinterpret_cast<uintptr_t>(bgr) & 3) == 0 && (reinterpret_cast<uintptr_t>(flow) & 15) == 0;
-    hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned int) * (kMaxStride * (size_t)n + 1), s);
+    const unsigned bx = (unsigned)((a.npix + kBpx - 1) / kBpx);
+    if (maxmotion > 0.0f) {  // fixed range: one colour pass over every field
+        a.flow = reinterpret_cast<const float2*>(flow);
+        a.bgr = bgr;
+        a.ws = ws;
+        hipLaunchKernelGGL(k_color_px, dim3(bx, n), dim3(kThreads), 0, s, a);
+        return hipGetLastError();
+    }
+    hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned int) * kMaxStride * (size_t)n, s);
     if (e != hipSuccess) return e;
-    const long long items = (long long)(a.na + a.nb) * n;
-    if (items >= (1LL << 31)) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)std::min<long long>((items + kClaim - 1) / kClaim, 256 * 8);  // persistent: 8 per CU
-    hipLaunchKernelGGL(k_color, dim3(grid), dim3(kThreads), 0, s, a);
+    // fields per chunk: ~128 MB of flow, re-read from the Infinity Cache
+    const long long fbytes = a.npix * 8;
+    const int chunk = (int)std::max<long long>(1, std::min<long long>(n, (128LL << 20) / std::max(1LL, fbytes)));
+    const unsigned mb = (unsigned)std::min<long long>(256, (a.npix + 2LL * kThreads * 8 - 1) / (2LL * kThreads * 8));
+    for (int f0 = 0; f0 < n; f0 += chunk) {
+        const int nc = std::min(chunk, n - f0);
+        a.flow = reinterpret_cast<const float2*>(flow) + (size_t)f0 * a.npix;
+        a.bgr = bgr + (size_t)f0 * a.npix * 3;
+        a.ws = ws + (size_t)kMaxStride * f0;
+        hipLaunchKernelGGL(k_color_max, dim3(mb, nc), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL(k_color_px, dim3(bx, nc), dim3(kThreads), 0, s, a);
+    }
     return hipGetLastError();
 }
 
-size_t flow_color_ws_words(int n) { return (size_t)kMaxStride * n + 1; }
+size_t flow_color_ws_words(int n) { return (size_t)kMaxStride * n; }
 
 }  // namespace dis

@@ -419,19 +419,24 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
 }
 
 #ifndef DIS_HEAD
-#define DIS_HEAD 1  // the coarse head (levels at 8 lanes per patch) as one launch (k_search8_head)
+// the coarse head (levels at 8 lanes per patch) as one launch (k_search8_head)
+// by default; r04 step A/Bs against one launch per level (variant 7):
+// 1.431 / 1.423 and 1.416 / 1.402 ms -- the head's waiting blocks hold CU
+// slots the other sub-batch's search could use -- so off; variant 8 selects it
+#define DIS_HEAD 0
 #endif
 
 // Lowest level of the fused coarse head for a sub-batch of n pairs, or C + 1
 // when there is none: the run of levels C, C-1, ... that search at 8 lanes per
 // patch (at most kHeadMax, at least two), on the plain fast path (patch size
-// 8, no paper mode, refinement or debug dumps; variant 7 = auto without it).
+// 8, no paper mode, refinement or debug dumps). Variant 8 selects it, variant
+// 7 never uses it, the auto variant 0 when built with DIS_HEAD=1.
 int head_lo(const dis_ctx* c, int n)
 {
     const dis::Geometry& g = c->g;
     const int none = g.C + 1;
-    if (!DIS_HEAD || g.ps != 8 || c->variant == 1 || c->variant == 6 || c->variant == 7 || c->debug ||
-        c->p.paper_mode || c->p.var_refine_iters > 0 || !c->head_done)
+    const bool want = c->variant == 8 || (DIS_HEAD && c->variant != 1 && c->variant != 6 && c->variant != 7);
+    if (!want || g.ps != 8 || c->debug || c->p.paper_mode || c->p.var_refine_iters > 0 || !c->head_done)
         return none;
     int l = g.C;
     while (l >= g.F && g.C - l + 1 <= dis::kHeadMax &&
@@ -1328,7 +1333,7 @@ dis_status dis_set_precision(dis_ctx* c, int mode)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 7) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..7");
+    if (variant < 0 || variant > 8) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..8");
     c->variant = variant;
     return DIS_OK;
 }

@@ -576,7 +576,13 @@ struct BlockLds {
 // TSC: the LDS tile row stride as a compile-time constant (0: a.tile_stride at
 // run time). Constant, all 45 taps of an update come from one base address
 // plus ds_read immediate offsets (no per-row address arithmetic).
-template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false, int TSC = 0>
+// kXcd (k_search8_head): the coarser level's patch displacements were written
+// by other workgroups of the same launch, possibly on other XCDs, whose L2s
+// are not coherent: they are read, and this level's are written, as
+// agent-scope atomics (global_load / global_store sc1), so no L2 write-back
+// or invalidation fence is needed.
+template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false, int TSC = 0,
+          bool kXcd = false>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -635,7 +641,15 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         for (int k = 0; k < kCuPer<LPP>; ++k) {
             const int i = tid + k * NT;
             const int cx = floordiv_r(i, rph), cy = i - cx * PH;
-            cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
+            if constexpr (kXcd) {
+                unsigned long long v = 0;
+                if (i < PN)
+                    v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(uc + (ga + cx) * a.c_nph + ha + cy),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cuv[k] = __builtin_bit_cast(float2, v);
+            } else {
+                cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
+            }
         }
         if (tid < BX + kBY) {
             // covering coarse-patch range per block column / row (src/patch_grid.cpp:121-182
@@ -947,7 +961,15 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         u0 = q ? up : uv;
         u1 = q ? uv : up;
     }
-    if (active && q == 0) a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
+    if (active && q == 0) {
+        float2* const o = a.u_out + (size_t)pair * a.u_stride + gx * a.nph + gy;
+        if constexpr (kXcd)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(o),
+                               __builtin_bit_cast(unsigned long long, make_float2(u0, u1)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        else
+            *o = make_float2(u0, u1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1114,10 +1136,14 @@ k_search8(Search8Args a)
 // The coarse head in one launch (HeadArgs, dis_kernels.h): workgroup b runs
 // block (bx, by) of pair `pair` at head level i; level i > 0 first waits
 // until every block of the pair at level i - 1 has published its patch
-// displacements (agent-scope release / acquire: the levels' blocks run on any
-// XCD). Deadlock-free with in-order workgroup dispatch: a block waits only
-// for blocks of lower workgroup ids, which were dispatched before it and
-// never wait on it.
+// displacements. The blocks run on any XCD: the displacements and counters
+// are agent-scope atomics (search_block kXcd), and a block counts itself done
+// only after its stores are acknowledged (vmcnt 0) -- no agent-scope
+// release/acquire fences, whose L2 write-back / invalidation (buffer_wbl2 /
+// buffer_inv sc1) cost the co-running sub-batch its L2 contents (r04: the
+// step 11 % slower with them). Deadlock-free with in-order workgroup
+// dispatch: a block waits only for blocks of lower workgroup ids, which were
+// dispatched before it and never wait on it.
 template <bool kFma, int TSC>
 __global__ void __launch_bounds__(kThreads<8>) __attribute__((amdgpu_waves_per_eu(kWaves<8, true>)))
 k_search8_head(HeadArgs h)
@@ -1133,17 +1159,15 @@ k_search8_head(HeadArgs h)
         if (threadIdx.x == 0) {
             const int* d = h.done + (i - 1) * h.batch + pair;
             const int need = h.nbx[i - 1] * h.nby[i - 1];
-            while (__hip_atomic_load(d, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need)
+            while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
                 __builtin_amdgcn_s_sleep(1);
         }
         __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    search_block<8, true, false, kFma, false, TSC>(h.lv[i], bx, by, pair, S);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this thread's u stores, before the count
+    search_block<8, true, false, kFma, false, TSC, true>(h.lv[i], bx, by, pair, S);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's u stores acknowledged
     __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(h.done + i * h.batch + pair, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(h.done + i * h.batch + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list

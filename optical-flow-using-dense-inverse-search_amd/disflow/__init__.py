@@ -290,7 +290,8 @@ class DenseInverseSearch:
     def set_variant(self, variant: int) -> None:
         """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels,
         fused coarse head), 1 = generic only, 2 / 3 / 4 / 5 = 4 / 2 / 8 / 1 lanes per
-        patch, 6 = one wave per patch, 7 = auto with one launch per coarse level."""
+        patch, 6 = one wave per patch, 7 = auto with one launch per coarse level (the
+        default's form), 8 = auto with the coarse levels fused into one launch."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
 
     def set_concurrency(self, streams: int) -> None:

@@ -462,7 +462,7 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
     exp_fb = oracle.calc_from_params(J0, J1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
     for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64"),
-                          (7, "auto, no fused head")):
+                          (7, "auto, one launch per level"), (8, "auto, fused head")):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
@@ -471,11 +471,11 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
 HEAD_CASES = [
     # (W, H, preset, batch, streams, variant, fma): the fused coarse head
     # (k_search8_head) against the per-level launches (variant 7) and the oracle
-    (1920, 1080, "MEDIUM", 3, 1, 0, 0),   # levels 6..4 in one launch (3 pairs)
-    (1920, 1080, "MEDIUM", 4, 2, 0, 1),   # two sub-batches, tolerance mode (vs variant 7 only)
-    (640, 480, "ULTRAFAST", 5, 2, 0, 0),  # C 4 .. (levels at 8 lanes per patch)
-    (320, 240, "MEDIUM", 2, 1, 4, 0),     # every level at 8 lanes: the head reaches the finest level
-    (203, 151, "SLOW", 3, 3, 4, 0),       # ragged, F = 0, three sub-batches of one pair
+    (1920, 1080, "MEDIUM", 3, 1, 8, 0),   # levels 6..4 in one launch (3 pairs)
+    (1920, 1080, "MEDIUM", 4, 2, 8, 1),   # two sub-batches, tolerance mode (vs variant 7 only)
+    (640, 480, "ULTRAFAST", 5, 2, 8, 0),  # C 4 .. (levels at 8 lanes per patch)
+    (320, 240, "MEDIUM", 2, 1, 8, 0),     # every level at 8 lanes: the head reaches the finest level
+    (203, 151, "SLOW", 3, 3, 8, 0),       # ragged, F = 0, three sub-batches of one pair
 ]
 
 
@@ -492,9 +492,9 @@ def test_fused_head_bitexact(disflow_mod, oracle, W, H, preset, B, streams, vari
     eng.set_precision(fma)
     eng.set_variant(variant)
     got = eng.calc_batch(I0, I1)
-    eng.set_variant(7 if variant == 0 else 3)  # per-level launches (variant 3: 2 lanes everywhere)
+    eng.set_variant(7 if variant == 8 else 3)  # per-level launches (variant 3: 2 lanes everywhere)
     ref = eng.calc_batch(I0, I1)
-    if variant == 0:
+    if variant == 8:
         _assert_bitexact(got, ref, "fused head vs per-level launches")
     if not fma:
         for k in range(B):

@@ -85,6 +85,12 @@ def main():
         t = times[v]
         print(f"{v:70s} median {statistics.median(t):.3f} ms  min {min(t):.3f} ms  "
               f"pairs/s {B / statistics.median(t) * 1e3:.0f}  same_as_first={same}")
+    # each context is destroyed by the library that created it (a context
+    # handed to another build's dis_destroy crashed the process at exit)
+    torch.cuda.synchronize()
+    for v, L, eng in engines:
+        disflow._lib = L
+        eng.close()
 
 
 def spawn(a):

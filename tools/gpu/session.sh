@@ -12,6 +12,7 @@
 #   smoke                        __graft_entry__.smoke()
 #   tool=<name> [args]           a built tools/ binary (e.g. tool=issue_mix)
 #   py=<script> [args]           a python script of the repo (e.g. py="tools/bench_configs.py --configs colour")
+#   prof=<script> [args]         the same under rocprofv3 --kernel-trace --stats: top kernels by total time
 # Libraries are paths relative to the package's disflow/ (e.g. libdis_hip_x.so);
 # build variants first on the CPU: tools/build_variants.sh name:"-DFLAG=1".
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
@@ -38,6 +39,16 @@ for s in "$@"; do
     smoke) run s${n}_smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tool) run s${n}_$(echo "$v" | cut -d' ' -f1) 300 ./tools/$v ;;
     py) run s${n}_$(basename "$(echo "$v" | cut -d' ' -f1)" .py) 600 python3 $v ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$GRAFT_REPO_ROOT/gpurun_out/prof_s$n" -o run -- python3 "$GRAFT_REPO_ROOT"/$v) > gpurun_out/s${n}_prof.log 2>&1
+          rc=$?; echo "== s${n}_prof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/s${n}_prof.log; exit $rc; }
+          python3 - gpurun_out/prof_s$n/run_kernel_stats.csv <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:12]:
+    print(f"  {r['Name'][:60]:60s} calls {int(r['Calls']):6d}  avg {float(r['AverageNs']) / 1e3:9.2f} us  total {float(r['TotalDurationNs']) / 1e6:9.3f} ms")
+PY
+          ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
