@@ -63,8 +63,17 @@
 #ifndef DIS_TAP_PREFETCH_ROWS
 #define DIS_TAP_PREFETCH_ROWS 3
 #endif
+#ifndef DIS_RHS_ORDER
+#define DIS_RHS_ORDER 1  // iterate_split: lanes carry the pivoted right-hand sides (no per-update swap selects)
+#endif
+#ifndef DIS_TAP_ADDR2
+#define DIS_TAP_ADDR2 1  // iterate_split tile path, tolerance mode: byte-offset tap bases, VGPR row step
+#endif
 #ifndef DIS_RESET_OUT
 #define DIS_RESET_OUT 1  // iterate_split: the outlier reset applied once, after the loop, on the exiting lanes
+#endif
+#ifndef DIS_FMA_CENTER
+#define DIS_FMA_CENTER 1  // tolerance mode: centred template gradients instead of a per-update mean (see search_block)
 #endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
@@ -319,8 +328,11 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
             if constexpr (kFence) __builtin_amdgcn_sched_barrier(0);  // one row of taps in flight
         }
     }
-    if (norm) {
-        const float mean = patch_sum<LPP>(r) / 64.0f;  // sum / num_points_patch (:265)
+    // (tolerance mode: the mean is folded into centred gradients, search_block)
+    if (norm && !(kFma && DIS_FMA_CENTER)) {
+        // sum / num_points_patch (:265); x / 64 = x * 2^-6 exactly rounded either
+        // way, as v_ldexp (inline exponent) instead of a v_mul with a literal
+        const float mean = __builtin_amdgcn_ldexpf(patch_sum<LPP>(r), -6);
 #pragma unroll
         for (int j = 0; j < 8 * kNCol<LPP>; ++j) r[j] = r[j] - mean;
     }
@@ -400,6 +412,8 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
 }
 
 [[maybe_unused]] __device__ __forceinline__ float xor1f(float v) { return quad_perm<kQuadXor1>(v); }
+constexpr int kQuadEven = 0xA0;  // [0,0,2,2]: lanes 2k, 2k+1 read lane 2k
+constexpr int kQuadOdd = 0xF5;   // [1,1,3,3]: lanes 2k, 2k+1 read lane 2k+1
 [[maybe_unused]] __device__ __forceinline__ int xor1i(int v) { return __builtin_amdgcn_mov_dpp(v, kQuadXor1, 0xF, 0xF, true); }
 
 // The LPP-2 iteration with the per-patch scalar work split between the
@@ -432,7 +446,11 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
     float pv = sv;
     bool reset = false;  // DIS_RESET_OUT: the exit was an outlier / out-of-bounds reset
     const float ubv = q ? a.tmp_ub_h : a.tmp_ub_w;
-    const bool f = (lu.swap != 0) != (q != 0);  // c0 takes the partner's right-hand side
+    // DIS_RHS_ORDER: the caller arranged (g1, g2) so that lane 2k's own sum is
+    // the pivoted c0 and lane 2k+1's c1 (PartialPivLU's row swap folded into
+    // which gradient each lane carries); otherwise lane q's own sum is b_q and
+    // c0 takes the partner's when f
+    const bool f = (lu.swap != 0) != (q != 0);
     float r[32];
     const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;  // div_pre
     constexpr int PR = DIS_TAP_PREFETCH_ROWS;  // tap rows read ahead (the rest stream behind them)
@@ -498,9 +516,18 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         }
         float d0, c1;
         {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
-            float c0 = f ? bpart : bown;
-            c1 = f ? bown : bpart;
-            c1 = c1 - lu.l10 * c0;
+            float c0;
+            if constexpr (DIS_RHS_ORDER) {
+                (void)bpart;
+                (void)f;
+                c0 = quad_perm<kQuadEven>(bown);                                      // lane 2k's sum
+                c1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bown), kQuadOdd, 0xF, 0xF, true)) -
+                     lu.l10 * c0;                                                    // lane 2k+1's
+            } else {
+                c0 = f ? bpart : bown;
+                c1 = f ? bown : bpart;
+                c1 = c1 - lu.l10 * c0;
+            }
             if constexpr (kFma) {
                 c1 = c1 * r11;
                 c0 = __builtin_fmaf(-c1, lu.u01, c0);
@@ -517,7 +544,8 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         const float n2 = e2 + xor1f(e2);  // ex * ex + ey * ey
         // either coordinate out: the pair's OR, on the scalar unit (one ballot
         // per compare: each v_cmp writes its lane mask straight to SGPRs)
-        unsigned long long m = __builtin_amdgcn_ballot_w64(n2 > a.thr_sq) | __builtin_amdgcn_ballot_w64(n2 != n2) |
+        // !(n2 <= thr_sq): over the threshold or NaN in one compare
+        unsigned long long m = __builtin_amdgcn_ballot_w64(!(n2 <= a.thr_sq)) |
                                __builtin_amdgcn_ballot_w64(pv < a.tmp_lb) | __builtin_amdgcn_ballot_w64(pv > ubv);
         m |= ((m >> 1) & 0x5555555555555555ull) | ((m << 1) & 0xAAAAAAAAAAAAAAAAull);
         const bool bad = __builtin_amdgcn_inverse_ballot_w64(m);
@@ -823,14 +851,32 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         const float h11 = patch_dot<LPP, kFma>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
+    if constexpr (kFma && DIS_FMA_CENTER) {
+        // tolerance mode (summation order free within the stated tolerance):
+        // sum(g (r - mean r)) = sum((g - mean g) r), so the right-hand sides
+        // take gradients centred once per patch and the update loop skips the
+        // mean of the warped patch (src/patch.cpp:261-266) and its 32
+        // subtractions per lane -- the Hessian above keeps the raw gradients
+        if (a.norm) {
+            const float mx = patch_sum<LPP>(gdx) * (1.0f / 64), my = patch_sum<LPP>(gdy) * (1.0f / 64);
+#pragma unroll
+            for (int j = 0; j < 8 * NC; ++j) {
+                gdx[j] = gdx[j] - mx;
+                gdy[j] = gdy[j] - my;
+            }
+        }
+    }
     // LPP 2, split iteration (iterate_split): the y lane keeps (gy, gx)
     constexpr bool kSplit = LPP == 2 && DIS_SPLIT_PATCH && !kPhys;
+    // (DIS_RHS_ORDER: the lane whose right-hand side is b1 -- the y lane, or
+    // the x lane when the LU pivot swapped the rows -- keeps (gy, gx))
+    [[maybe_unused]] const bool own_y = DIS_RHS_ORDER ? (lu.swap != 0) != (q != 0) : q != 0;
     if constexpr (kSplit) {
 #pragma unroll
         for (int j = 0; j < 8 * NC; ++j) {
             const float x = gdx[j], y = gdy[j];
-            gdx[j] = q ? y : x;
-            gdy[j] = q ? x : y;
+            gdx[j] = own_y ? y : x;
+            gdy[j] = own_y ? x : y;
         }
     }
     const float sx = rx + ix, sy = ry + iy;
@@ -896,10 +942,36 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // partner's by one DPP add
                 const int M = q ? TS : 1, K = q ? -(5 + ty0) * TS : -(5 + tx0);
                 const float* tq = tile + 4 * q;
+#if DIS_TAP_ADDR2
+                // (kFma) byte offsets: t = cv * 4M + 4K, the pair's sum by one DPP
+                // add, the three row-group bases (ds_read2 immediates <= 255
+                // dwords) by adding a VGPR-held 3-row step: 5 address VALU per
+                // update instead of 7, no literal operands
+                const int M4 = 4 * M, K4 = 4 * K;
+                const char* const tqb = reinterpret_cast<const char*>(tq);
+                // three rows, in bytes: a loop-invariant VGPR operand instead of a
+                // literal (tolerance mode only: the exact kernel is at 128 VGPRs
+                // and spilled; with literals its loop grew 463 -> 470 VALU)
+                int g3 = 12 * TS;
+                __asm__("" : "+v"(g3));
+#endif
                 iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, (kFma ? DIS_TAP_PREFETCH_FMA : DIS_TAP_PREFETCH) != 0>(
                                                                              a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
-                                                                             q ? bt1 : bt0, &uv,
+                                                                             own_y ? bt1 : bt0, &uv,
                                                    [&](int cv) {
+#if DIS_TAP_ADDR2
+                                                     if constexpr (kFma) {
+                                                       const int tb = __mul24(cv, M4) + K4;
+                                                       const char* const c0 = tqb + (tb + xor1i(tb));
+                                                       const float *f0 = reinterpret_cast<const float*>(c0),
+                                                                   *f1 = reinterpret_cast<const float*>(c0 + g3),
+                                                                   *f2 = reinterpret_cast<const float*>(c0 + g3 + g3);
+                                                       return [=](int k, int c) {
+                                                           return k < 3 ? f0[k * TS + c]
+                                                                        : k < 6 ? f1[(k - 3) * TS + c] : f2[(k - 6) * TS + c];
+                                                       };
+                                                     } else {
+#endif
                                                        const int t = __mul24(cv, M) + K;
                                                        // three row groups, each one base register and
                                                        // ds_read2 immediates (<= 255 dwords); opaque to the
@@ -913,6 +985,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                                                            return k < 3 ? b0[k * TS + c]
                                                                         : k < 6 ? b1[(k - 3) * TS + c] : b2[(k - 6) * TS + c];
                                                        };
+#if DIS_TAP_ADDR2
+                                                     }
+#endif
                                                    });
             }
         } else if (valid) {
@@ -929,7 +1004,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     } else if constexpr (kFallback) {
         if constexpr (kSplit) {
             if (valid) {
-                iterate_split<true, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, q ? bt1 : bt0, &uv,
+                iterate_split<true, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, own_y ? bt1 : bt0, &uv,
                                                   [&](int cv) {
                                                       const int cp = xor1i(cv);
                                                       const int y0 = (q ? cv : cp) - 5, x0 = (q ? cp : cv) - 5 + 4 * q;
