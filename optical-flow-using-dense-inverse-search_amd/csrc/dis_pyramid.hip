@@ -306,165 +306,6 @@ __global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_e
     if constexpr (RW > 3) level_row(std::integral_constant<int, 3>{});
 }
 
-#ifndef DIS_PYR12_ROLL
-#define DIS_PYR12_ROLL 0  // > 0: k_pyr12_roll, that many level-2 rows per wave
-#endif
-#ifndef DIS_PYR12_ROLL_PF
-#define DIS_PYR12_ROLL_PF 1  // k_pyr12_roll: the next row's four u8 rows in flight during this row's arithmetic
-#endif
-#if DIS_PYR12_ROLL
-// k_pyr12 walking DIS_PYR12_ROLL consecutive level-2 rows per wave: the
-// window of level-2 row y2 is level-0 rows 4 y2 - 1 .. 4 y2 + 4, so the next
-// row's window shares two rows with it; they stay in registers and only four
-// new u8 rows are read per level-2 row (1 + 0.5 / ROLL of the frame bytes
-// instead of 1.5x with one row per wave, whatever order the waves run in).
-// Same lane layout, halo handling and arithmetic as k_pyr12.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12_roll(PyramidArgs a)
-{
-    constexpr int NR = 6, RR = DIS_PYR12_ROLL;
-    const int lane = threadIdx.x;
-    const int W2 = a.w[2], H2 = a.Hp >> 2;
-    const int bx = blockIdx.x, bz = blockIdx.z;
-    const int y2b = RR * blockIdx.y;
-    const int g = bx * 64 + lane;
-    const int pair = bz >> 1, frame = bz & 1;
-    if (bx == 0 && blockIdx.y == 0 && bz == 0) {
-        if (lane < a.nzero) a.zero[lane] = 0;
-        for (int i = lane; i < a.nzero2; i += 64) a.zero2[i] = 0;
-    }
-    const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-    const int ng = (W2 + 3) >> 2;
-    const int gc = g < ng ? g : ng - 1;
-    const int x0 = 16 * gc;
-    const bool body = a.qword_ok && x0 >= a.pl && x0 + 15 - a.pl <= a.W - 1;
-    const bool nb_l = body && lane > 0 && x0 - 16 >= a.pl;
-    const bool nb_r = body && lane < 63 && x0 + 31 - a.pl <= a.W - 1 && g + 1 < ng;
-    const bool vec = a.qword_ok && a.W >= 16;
-    const int xb = body ? x0 - a.pl : 0;
-    const int cl = src_col(a, x0 - 1), cr = src_col(a, x0 + 16);
-    unsigned d[4][NR], wl[NR], wr[NR];
-    uint4 v[NR];
-    // issue the loads of window rows R0 .. NR-1 of level-2 row y2 (all in
-    // flight together), then (finish) unpack them, gather the bytes of the
-    // lanes without a 16-byte body and form the halo columns
-    auto issue = [&](auto r0_c, int y2) {
-        constexpr int R0 = decltype(r0_c)::value;
-        if (vec) {
-#pragma unroll
-            for (int r = R0; r < NR; ++r)
-                v[r] = *reinterpret_cast<const uint4*>(in + (size_t)src_row(a, 4 * y2 - 1 + r) * a.stride + xb);
-        }
-    };
-    auto finish = [&](auto r0_c, int y2) {
-        constexpr int R0 = decltype(r0_c)::value;
-        const uint8_t* rows[NR];
-#pragma unroll
-        for (int r = R0; r < NR; ++r) rows[r] = in + (size_t)src_row(a, 4 * y2 - 1 + r) * a.stride;
-        if (vec) {
-#pragma unroll
-            for (int r = R0; r < NR; ++r) {
-                d[0][r] = v[r].x;
-                d[1][r] = v[r].y;
-                d[2][r] = v[r].z;
-                d[3][r] = v[r].w;
-            }
-        }
-        if (!body) {
-            int xo = x0;  // opaque per row set: the 16 column indices are not hoisted out of the row loop
-            __asm__("" : "+v"(xo));
-#pragma unroll
-            for (int r = R0; r < NR; ++r)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    unsigned w = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) w |= (unsigned)rows[r][src_col(a, xo + 4 * k + b)] << (8 * b);
-                    d[k][r] = w;
-                }
-        }
-#pragma unroll
-        for (int r = R0; r < NR; ++r) {
-            wl[r] = wave_shr1(d[3][r], 0u);
-            wr[r] = wave_shl1(d[0][r], 0u);
-        }
-        if (!nb_l || !nb_r) {
-#pragma unroll
-            for (int r = R0; r < NR; ++r) {
-                const unsigned hl = rows[r][cl], hr = rows[r][cr];
-                if (!nb_l) wl[r] = hl << 24;
-                if (!nb_r) wr[r] = hr;
-            }
-        }
-    };
-    float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
-    const int np = min(4, W2 - 4 * g);
-    auto level_row = [&](int y2) {
-        float l1row[2][8], l2v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            Block4 o;
-            block4<0, NR>(q == 0 ? wl : d[q - 1], d[q], q == 3 ? wr : d[q + 1], o);
-            if (a.write_l0 && q < np) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    *reinterpret_cast<float4*>(planes + (size_t)(4 * y2 + r) * a.Wp + x0 + 4 * q) =
-                        make_float4(o.m[r][0] * 0.125f, o.m[r][1] * 0.125f, o.m[r][2] * 0.125f, o.m[r][3] * 0.125f);
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                l1row[i][2 * q] = o.l1[i][0];
-                l1row[i][2 * q + 1] = o.l1[i][1];
-            }
-            l2v[q] = o.l2;
-        }
-        if (g >= ng) return;
-        float* p1 = planes + a.off[1] + (size_t)(2 * y2) * a.w[1] + 8 * g;
-        float* p2 = planes + a.off[2] + (size_t)y2 * W2 + 4 * g;
-        if (np == 4 && a.vec_st) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1]) =
-                    make_float4(l1row[i][0], l1row[i][1], l1row[i][2], l1row[i][3]);
-                *reinterpret_cast<float4*>(p1 + (size_t)i * a.w[1] + 4) =
-                    make_float4(l1row[i][4], l1row[i][5], l1row[i][6], l1row[i][7]);
-            }
-            *reinterpret_cast<float4*>(p2) = make_float4(l2v[0], l2v[1], l2v[2], l2v[3]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (q < np) {
-                    p1[2 * q] = l1row[0][2 * q];
-                    p1[2 * q + 1] = l1row[0][2 * q + 1];
-                    p1[a.w[1] + 2 * q] = l1row[1][2 * q];
-                    p1[a.w[1] + 2 * q + 1] = l1row[1][2 * q + 1];
-                    p2[q] = l2v[q];
-                }
-        }
-    };
-    issue(std::integral_constant<int, 0>{}, y2b);
-    finish(std::integral_constant<int, 0>{}, y2b);
-    for (int y2 = y2b;;) {
-        const bool more = y2 + 1 < y2b + RR && y2 + 1 < H2;  // wave-uniform
-        if (DIS_PYR12_ROLL_PF && more) issue(std::integral_constant<int, 2>{}, y2 + 1);
-        level_row(y2);
-        if (!more) break;
-        ++y2;
-        // rows 4 y2 - 1, 4 y2 of the new window are the old window's last two
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            d[k][0] = d[k][4];
-            d[k][1] = d[k][5];
-        }
-        wl[0] = wl[4];
-        wl[1] = wl[5];
-        wr[0] = wr[4];
-        wr[1] = wr[5];
-        if (!DIS_PYR12_ROLL_PF) issue(std::integral_constant<int, 2>{}, y2);
-        finish(std::integral_constant<int, 2>{}, y2);
-    }
-}
-#endif
-
 // grid: (W2 / T2, H2 / T2, 2 * batch), T2 = 2^(L-2) level-2 pixels per tile
 // edge; one wave per tile computes levels 3..L in LDS
 #ifndef DIS_TAIL_TPW
@@ -622,13 +463,7 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     // offsets are multiples of 4: Wp, Hp % 4 == 0): 16-byte stores need W_2 % 4 == 0
     // (with C = 2 or 3, Wp is only a multiple of 4 or 8)
     b.vec_st = W2 % 4 == 0;
-#if DIS_PYR12_ROLL
-    (void)nrw;
-    DIS_LAUNCH(t, k_pyr12_roll, dim3((W2 + 255) / 256, (H2 + DIS_PYR12_ROLL - 1) / DIS_PYR12_ROLL, 2 * batch), dim3(64),
-               0, s, b);
-#else
     DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (nrw + kPyrWG - 1) / kPyrWG, 2 * batch), dim3(64 * kPyrWG), 0, s, b);
-#endif
 #ifndef DIS_TAIL_REG
 #define DIS_TAIL_REG 1
 #endif

@@ -75,6 +75,15 @@
 #ifndef DIS_FMA_CENTER
 #define DIS_FMA_CENTER 1  // tolerance mode: centred template gradients instead of a per-update mean (see search_block)
 #endif
+#ifndef DIS_FMA_FUSED
+#define DIS_FMA_FUSED 1  // tolerance mode, LPP 2: warp fused into the dot products (iterate_split)
+#endif
+#ifndef DIS_FMA_FENCE
+#define DIS_FMA_FENCE 1  // fused loop: taps streamed row by row (109 VGPRs instead of 128 + a spill; r04 A/B 1.015 vs 1.031 ms)
+#endif
+#ifndef DIS_FMA_WAVES
+#define DIS_FMA_WAVES 4  // min waves per SIMD of the tolerance-mode LPP-2 tile kernel
+#endif
 #ifndef DIS_SEARCH8_WAVES
 #define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
 #endif
@@ -89,7 +98,10 @@ constexpr int kBX = LPP == 1 ? 16 : 8;
 constexpr int kBY = 8;
 template <int LPP>
 constexpr int kThreads = kBX<LPP> * kBY * LPP;
-constexpr int kTileH = 64;  // max staged tile rows
+#ifndef DIS_TILE_H
+#define DIS_TILE_H 64
+#endif
+constexpr int kTileH = DIS_TILE_H;  // max staged tile rows
 template <int LPP>
 constexpr int kTileW = LPP == 1 ? 96 : 64;  // max staged tile columns
 #ifndef DIS_TSMAX2
@@ -441,6 +453,7 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
                                               float* puv, TapAt&& tap_at)
 {
     auto mac = [](float acc, float x, float y) { return kFma ? __builtin_fmaf(x, y, acc) : acc + x * y; };
+    constexpr bool kFused = kFma && DIS_FMA_CENTER && DIS_FMA_FUSED && !kPrefetch;
     float uv = iv;
     const float sv = rv + uv;
     float pv = sv;
@@ -493,21 +506,51 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
             auto tap = tap_at(cvl);
             warp_patch<2, kFence, kFma>(w, a.norm, [&](int k, int c) { return k < PR ? T[k < PR ? k : 0][c] : tap(k, c); },
                                         r);
-        } else {
+        } else if constexpr (!kFused) {
             warp_patch<2, kFence, kFma>(w, a.norm, tap_at(cv), r);
         }
-        float C[4];
+        float bown;  // lane 2k: its own right-hand side, 2k+1: its own
+        if constexpr (kFused) {
+            // tolerance mode with centred gradients (no mean of the warped
+            // patch): each warped pixel goes straight into the two dot products,
+            // no residual array (fewer VGPRs), per-column accumulators summed
+            // in-lane, one cross-lane add per right-hand side
+            auto tap = tap_at(cv);
+            float x[4], y[4], prev[5], cur[5];
 #pragma unroll
-        for (int ci = 0; ci < 4; ++ci) {
-            float x = g1[8 * ci] * r[8 * ci], y = g2[8 * ci] * r[8 * ci];
+            for (int c = 0; c < 5; ++c) prev[c] = tap(0, c);
 #pragma unroll
-            for (int j = 1; j < 8; ++j) {
-                x = mac(x, g1[8 * ci + j], r[8 * ci + j]);
-                y = mac(y, g2[8 * ci + j], r[8 * ci + j]);
+            for (int j = 0; j < 8; ++j) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) cur[c] = tap(j + 1, c);
+#pragma unroll
+                for (int ci = 0; ci < 4; ++ci) {
+                    float t = w.w3 * cur[ci + 1];
+                    t = __builtin_fmaf(w.w2, cur[ci], t);
+                    t = __builtin_fmaf(w.w1, prev[ci + 1], t);
+                    t = __builtin_fmaf(w.w0, prev[ci], t);
+                    x[ci] = j ? __builtin_fmaf(g1[8 * ci + j], t, x[ci]) : g1[8 * ci] * t;
+                    y[ci] = j ? __builtin_fmaf(g2[8 * ci + j], t, y[ci]) : g2[8 * ci] * t;
+                }
+#pragma unroll
+                for (int c = 0; c < 5; ++c) prev[c] = cur[c];
+                if constexpr (DIS_FMA_FENCE) __builtin_amdgcn_sched_barrier(0);  // taps streamed row by row
             }
-            C[ci] = x + xor1f(y);
+            bown = ((x[0] + x[1]) + (x[2] + x[3])) + xor1f((y[0] + y[1]) + (y[2] + y[3]));
+        } else {
+            float C[4];
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) {
+                float x = g1[8 * ci] * r[8 * ci], y = g2[8 * ci] * r[8 * ci];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) {
+                    x = mac(x, g1[8 * ci + j], r[8 * ci + j]);
+                    y = mac(y, g2[8 * ci + j], r[8 * ci + j]);
+                }
+                C[ci] = x + xor1f(y);
+            }
+            bown = (C[0] + C[2]) + (C[1] + C[3]);  // lane 0: b0, lane 1: b1
         }
-        float bown = (C[0] + C[2]) + (C[1] + C[3]);  // lane 0: b0, lane 1: b1
         if constexpr (kPaper) bown = bown - btv;
         const float bpart = xor1f(bown);
         if constexpr (kPrefetch) {  // the next update's taps, in flight during the solve
@@ -578,8 +621,8 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
 #ifndef DIS_EXP_NO_FB
 #define DIS_EXP_NO_FB 0  // experiment: no k_search8_fb launches (wrong values if a list is not empty)
 #endif
-template <int LPP, bool kFallback>
-constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? DIS_FB_WAVES : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
+template <int LPP, bool kFallback, bool kFma = false>
+constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? DIS_FB_WAVES : kFma ? DIS_FMA_WAVES : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
 
 // LDS of one workgroup (block of patches)
 template <int LPP>
@@ -1186,7 +1229,7 @@ __global__ void __launch_bounds__(256) k_search_wave(Search8Args a)
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
 template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false, bool kPhys = false, int TSC = 0>
-__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback, kFma>)))
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;

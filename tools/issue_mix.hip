@@ -30,6 +30,10 @@
 #define CMP_S(i) "v_cmp_gt_f32 vcc, %9, %" #i "\n"
 #define CMP_V(i) "v_cmp_gt_f32 vcc, %8, %" #i "\n"
 #define CMPX(i) "v_cmp_gt_f32_e64 s[20:21], %" #i ", %8\n"
+// compare + select pairs, as the compiler emits `c ? a : b` (VCC, or an SGPR pair)
+#define CMPSEL_VCC(i) "v_cmp_gt_f32 vcc, %8, %" #i "\nv_cndmask_b32_e32 %" #i ", %" #i ", %8, vcc\n"
+#define CMPSEL_S(i) "v_cmp_gt_f32_e64 s[20:21], %8, %" #i "\nv_cndmask_b32_e64 %" #i ", %" #i ", %8, s[20:21]\n"
+#define CND_VCC64(i) "v_cndmask_b32_e64 %" #i ", %" #i ", %8, vcc\n"
 // 1 op of a kind, then 3 plain v_mul (the mix the loop has at worst)
 #define MIX(K) K(0) MUL_VV(1) MUL_VV(2) MUL_VV(3) K(4) MUL_VV(5) MUL_VV(6) MUL_VV(7)
 
@@ -54,6 +58,8 @@ __global__ void __launch_bounds__(256) k_mix(float* out, int kind, int iters, fl
     const unsigned long long mask = 0x5555555555555555ull;
     int vmask = (t & 1) ? -1 : 0;
     __asm__("" : "+v"(vmask));
+    // VCC defined before any kind reads it (as a VALU compare would leave it)
+    __asm__ volatile("v_cmp_gt_f32 vcc, %0, %1" ::"v"(m), "v"(c) : "vcc");
     KIND(0, V8(MUL_VV))
     KIND(1, V8(MUL_VS))
     KIND(2, V8(MUL_VL))
@@ -76,6 +82,10 @@ __global__ void __launch_bounds__(256) k_mix(float* out, int kind, int iters, fl
     KIND(19, MIX(BFI))
     KIND(20, MIX(CMP_S))
     KIND(21, MIX(ADD_ROR))
+    KIND(22, MIX(CND_VCC))
+    KIND(23, V8(CMPSEL_VCC))
+    KIND(24, V8(CMPSEL_S))
+    KIND(25, V8(CND_VCC64))
     out[t] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
 }
 
@@ -84,7 +94,8 @@ static const char* kNames[] = {"v_mul v,v",       "v_mul s,v",      "v_mul lit,v
                                "v_bfi v,v,v",     "v_fma v,v,v",    "v_fmac",        "v_mad_i32_i24",
                                "v_cmp s,v ->vcc", "v_cmp v,v ->vcc", "v_cmp ->s[]",  "mix 1:3 mul s,v",
                                "mix 1:3 mul lit", "mix 1:3 mul_dpp", "mix 1:3 cndmask s", "mix 1:3 bfi",
-                               "mix 1:3 cmp s", "mix 1:3 add_dpp ror8"};
+                               "mix 1:3 cmp s", "mix 1:3 add_dpp ror8", "mix 1:3 cndmask vcc",
+                               "cmp->vcc + cndmask vcc", "cmp->s[] + cndmask s[]", "v_cndmask_e64 vcc"};
 
 int main(int argc, char** argv)
 {
