@@ -1,16 +1,20 @@
 // dis_color.hip -- Middlebury flow colour coding:
 // draw_optical_flow / compute_color, src/color_coding.cpp:13-117.
 //
-// Two kernels over a batch of n W x H (u,v) fields (k_color_max, k_color_px):
-// per field the motion range (maxrad = max(1, max |u| over valid pixels),
-// :88-104) and then every pixel to BGR u8 (:106-115; invalid pixels stay
-// black). The float expressions are the reference's, in its order,
-// -ffp-contract=off (the division by maxrad correctly rounded through the
-// field's reciprocal, div_pre: the same bits); the one
-// library call, atan2f (:52), is restated as a fixed float algorithm (range
-// reduction to [0, 1] + the minimax polynomial of ARM's optimized-routines
-// atanf, <= 3 ulp) evaluated identically here and in the oracle. (The
-// reference's MSVC atan2f is unknown: unpinned.)
+// Per chunk of fields, two passes over a batch of n W x H (u,v) fields:
+// the motion range (maxrad = max(1, max |u| over valid pixels), :88-104; kept
+// as the largest squared radius, sqrtf taken once: sqrtf is monotone) and
+// then every pixel to BGR u8 (:106-115; invalid pixels stay black), the
+// colour pass of one chunk in the same launch as the max pass of the next
+// (k_color_step). The float expressions are the reference's, in its order,
+// -ffp-contract=off; the divisions and square roots are correctly rounded
+// (the field's division through its reciprocal, div_pre; atan2's min/max
+// quotient and the radius through the IEEE sequences' cores on the operand
+// ranges where those are exact, the IEEE operations elsewhere): the same
+// bits. The one library call, atan2f (:52), is restated as a fixed float
+// algorithm (range reduction to [0, 1] + the minimax polynomial of ARM's
+// optimized-routines atanf, <= 3 ulp) evaluated identically here and in the
+// oracle. (The reference's MSVC atan2f is unknown: unpinned.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,13 +53,56 @@ constexpr Wheel make_wheel()
 
 __constant__ Wheel c_wheel = make_wheel();  // read-only table: scalar/constant cache loads
 
+// a / b, correctly rounded, for 2^-60 <= b <= 2^60 and a = 0 or
+// b 2^-30 <= a <= b: the core of the IEEE division sequence (reciprocal, one
+// Newton step, quotient, two remainder corrections -- v_div_scale /
+// v_div_fmas / v_div_fixup without their scaling and special cases, which
+// these operands never need: the same bits). kFast: that core, clearing `ok`
+// outside its domain; otherwise the IEEE division.
+template <bool kFast>
+__device__ __forceinline__ float div_rn(float a, float b, bool& ok)
+{
+    if constexpr (!kFast) return a / b;
+    ok = ok && b >= 0x1p-60f && b <= 0x1p60f && (a == 0.0f || (a >= b * 0x1p-30f && a <= b));
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    float q = a * y;
+    float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// sqrtf(x), correctly rounded, for x = +0 or 2^-96 <= x <= 2^96: v_sqrt_f32
+// (within one ulp) and the residual tests of both neighbours (exact: see
+// dis_device.h sqrt_cr; no denormal scaling in this range). x here is a sum
+// of squares (never -0). kFast: that, clearing `ok` outside the range;
+// otherwise the IEEE sqrtf.
+template <bool kFast>
+__device__ __forceinline__ float sqrt_rn(float x, bool& ok)
+{
+    if constexpr (!kFast) return sqrtf(x);
+    ok = ok && ((x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f);
+    const float r = __builtin_amdgcn_sqrtf(x);
+    const float rm = __int_as_float(__float_as_int(r) - 1);
+    const float rp = __int_as_float(__float_as_int(r) + 1);
+    float y = __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
+    y = __builtin_fmaf(-rp, r, x) > 0.0f ? rp : y;
+    return x == 0.0f ? x : y;
+}
+
 // atan2(y, x) for finite y, x: t = min/max in [0, 1], atan(t) = t + t z P(z),
 // z = t^2 (ARM optimized-routines atanf coefficients), then the octant fix-up.
-__device__ __forceinline__ float atan2_dis(float y, float x)
+template <bool kFast>
+__device__ __forceinline__ float atan2_dis(float y, float x, bool& ok)
 {
     const float ax = fabsf(x), ay = fabsf(y);
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float t = mx > 0.0f ? mn / mx : 0.0f;
+    bool okd = true;
+    const float q = div_rn<kFast>(mn, mx, okd);
+    ok = ok && (okd || !(mx > 0.0f));
+    const float t = mx > 0.0f ? q : 0.0f;
     const float z = t * t;
     float p = 0x1.01fd88p-8f;
     p = p * z + -0x1.4c3c60p-6f;
@@ -74,7 +121,7 @@ __device__ __forceinline__ float atan2_dis(float y, float x)
 // is_flow_correct (src/color_coding.cpp:8-11)
 __device__ __forceinline__ bool flow_ok(float x, float y)
 {
-    return !(x != x) && !(y != y) && fabsf(x) < 1e9f && fabsf(y) < 1e9f;
+    return fabsf(x) < 1e9f && fabsf(y) < 1e9f;  // a NaN fails the compare: !isnan(x) && ... implied
 }
 
 constexpr int kMaxStride = 32;  // per field: [0] max radius bits (one 128-B line per field)
@@ -95,15 +142,19 @@ __device__ __forceinline__ float div_field(float u, float m, float rm, bool fast
 // with compute_color (:13-79) -> packed B | G << 8 | R << 16 (0 when invalid:
 // dst.setTo(0), :87). `col` = the wheel as floats (c_wheel / 255.f, the same
 // IEEE quotients the reference forms per pixel).
-__device__ __forceinline__ unsigned color_px(float2 u, float maxrad, float rmax, bool fast, const float4* col)
+// kFast: the division and sqrt fast paths above, `ok` cleared when an operand
+// is outside their domain (the caller then recomputes the pixel with
+// kFast = false: the IEEE operations, the same bits either way)
+template <bool kFast>
+__device__ __forceinline__ unsigned color_px(float2 u, float maxrad, float rmax, bool fast, const float4* col, bool& ok)
 {
     if (!flow_ok(u.x, u.y)) return 0u;
     const float fx = div_field(u.x, maxrad, rmax, fast), fy = div_field(u.y, maxrad, rmax, fast);  // (:113)
-    const float rad = sqrtf(fx * fx + fy * fy);
+    const float rad = sqrt_rn<kFast>(fx * fx + fy * fy, ok);
     // atan2(...) / (float)CV_PI, correctly rounded through RN(1 / pi) (div_pre)
     // on its domain, the IEEE division for |t| < 2^-60
     constexpr float kPi = 3.14159274f, kRPi = 1.0f / kPi;
-    const float t = atan2_dis(-fy, -fx);
+    const float t = atan2_dis<kFast>(-fy, -fx, ok);
     const float a = div_field(t, kPi, kRPi, true);
     const float fk = (a + 1.0f) / 2.0f * (float)(kNCols - 1);
     const int k0 = (int)fk;
@@ -140,25 +191,25 @@ struct ColorArgs {
     int vec;             // float4 loads / dwordx3 stores (npix % 4 == 0, aligned pointers)
 };
 
-// grid (blocks, fields): the valid-pixel max radius of each field (:88-104),
-// reduced per workgroup into one float-bit atomicMax (a max is
-// order-independent: exact)
-__global__ void __launch_bounds__(kThreads) k_color_max(ColorArgs a)
+// grid (blocks, fields): the valid-pixel max squared radius of each field
+// (:88-104; the colour pass takes its sqrtf), reduced per workgroup into one
+// float-bit atomicMax (a max is order-independent: exact; squares are >= +0,
+// so their bit patterns order like the values)
+__device__ __forceinline__ void color_max(const ColorArgs& a, int bx, int nbx, int f)
 {
     __shared__ float red[kThreads / 64];
-    const int f = blockIdx.y;
     const float2* fl = a.flow + (size_t)f * a.npix;
     float m = 0.0f;
-    const long long step = 2LL * kThreads * gridDim.x;
-    for (long long i = 2LL * ((long long)blockIdx.x * kThreads + threadIdx.x); i < a.npix; i += step) {
+    const long long step = 2LL * kThreads * nbx;
+    for (long long i = 2LL * ((long long)bx * kThreads + threadIdx.x); i < a.npix; i += step) {
         if (a.vec && i + 2 <= a.npix) {
             const float4 u = *reinterpret_cast<const float4*>(fl + i);
-            if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));  // (:101)
-            if (flow_ok(u.z, u.w)) m = fmaxf(m, sqrtf(u.z * u.z + u.w * u.w));
+            if (flow_ok(u.x, u.y)) m = fmaxf(m, u.x * u.x + u.y * u.y);  // (:101), squared
+            if (flow_ok(u.z, u.w)) m = fmaxf(m, u.z * u.z + u.w * u.w);
         } else {
             for (long long q = i; q < i + 2 && q < a.npix; ++q) {
                 const float2 u = fl[q];
-                if (flow_ok(u.x, u.y)) m = fmaxf(m, sqrtf(u.x * u.x + u.y * u.y));
+                if (flow_ok(u.x, u.y)) m = fmaxf(m, u.x * u.x + u.y * u.y);
             }
         }
     }
@@ -171,20 +222,22 @@ __global__ void __launch_bounds__(kThreads) k_color_max(ColorArgs a)
 
 // grid (ceil(npix / kBpx), fields): each lane colours kBG groups of 4
 // consecutive pixels, all its loads in flight before any is consumed
-__global__ void __launch_bounds__(kThreads) k_color_px(ColorArgs a)
+__device__ __forceinline__ void color_pixels(const ColorArgs& a, int bx, int f)
 {
     __shared__ float4 col[kNCols];  // the wheel as floats, one 16-byte entry per colour
     for (int i = threadIdx.x; i < kNCols; i += kThreads)
         col[i] = make_float4((float)c_wheel.rgb[i][0] / 255.f, (float)c_wheel.rgb[i][1] / 255.f,
                              (float)c_wheel.rgb[i][2] / 255.f, 0.0f);
     __syncthreads();
-    const int f = blockIdx.y;
     const float2* fl = a.flow + (size_t)f * a.npix;
     // maxrad = maxmotion, or max(1, max radius) when maxmotion <= 0 (:88-104)
-    const float maxrad = a.maxmotion > 0.0f ? a.maxmotion : fmaxf(1.0f, __uint_as_float(a.ws[(size_t)kMaxStride * f]));
+    // (the max pass keeps the largest squared radius: sqrtf is monotone, so
+    // sqrtf of it is the largest radius, :101, bit for bit)
+    const float maxrad =
+        a.maxmotion > 0.0f ? a.maxmotion : fmaxf(1.0f, sqrtf(__uint_as_float(a.ws[(size_t)kMaxStride * f])));
     const bool fast = maxrad >= 0x1p-60f && maxrad <= 0x1p60f;
     const float rmax = 1.0f / maxrad;
-    const long long pb = (long long)blockIdx.x * kBpx + 4 * threadIdx.x;
+    const long long pb = (long long)bx * kBpx + 4 * threadIdx.x;
     uint8_t* const out = a.bgr + (size_t)f * a.npix * 3;
     if (a.vec && pb + 4 * kThreads * (kBG - 1) + 4 <= a.npix) {
         float4 v[kBG][2];
@@ -197,10 +250,17 @@ __global__ void __launch_bounds__(kThreads) k_color_px(ColorArgs a)
 #pragma unroll
         for (int g = 0; g < kBG; ++g) {
             const long long p0 = pb + 4 * kThreads * g;
-            const unsigned c0 = color_px(make_float2(v[g][0].x, v[g][0].y), maxrad, rmax, fast, col);
-            const unsigned c1 = color_px(make_float2(v[g][0].z, v[g][0].w), maxrad, rmax, fast, col);
-            const unsigned c2 = color_px(make_float2(v[g][1].x, v[g][1].y), maxrad, rmax, fast, col);
-            const unsigned c3 = color_px(make_float2(v[g][1].z, v[g][1].w), maxrad, rmax, fast, col);
+            bool ok = true;
+            unsigned c0 = color_px<true>(make_float2(v[g][0].x, v[g][0].y), maxrad, rmax, fast, col, ok);
+            unsigned c1 = color_px<true>(make_float2(v[g][0].z, v[g][0].w), maxrad, rmax, fast, col, ok);
+            unsigned c2 = color_px<true>(make_float2(v[g][1].x, v[g][1].y), maxrad, rmax, fast, col, ok);
+            unsigned c3 = color_px<true>(make_float2(v[g][1].z, v[g][1].w), maxrad, rmax, fast, col, ok);
+            if (__builtin_expect(!ok, 0)) {  // an operand outside the fast domain: the IEEE operations
+                c0 = color_px<false>(make_float2(v[g][0].x, v[g][0].y), maxrad, rmax, fast, col, ok);
+                c1 = color_px<false>(make_float2(v[g][0].z, v[g][0].w), maxrad, rmax, fast, col, ok);
+                c2 = color_px<false>(make_float2(v[g][1].x, v[g][1].y), maxrad, rmax, fast, col, ok);
+                c3 = color_px<false>(make_float2(v[g][1].z, v[g][1].w), maxrad, rmax, fast, col, ok);
+            }
             // 4 pixels x 3 bytes, little-endian: c0 | c1 << 24, c1 >> 8 | c2 << 16, c2 >> 16 | c3 << 8
             *reinterpret_cast<uint3*>(out + p0 * 3) =
                 make_uint3(c0 | (c1 << 24), (c1 >> 8) | (c2 << 16), (c2 >> 16) | (c3 << 8));
@@ -209,12 +269,36 @@ __global__ void __launch_bounds__(kThreads) k_color_px(ColorArgs a)
         for (int g = 0; g < kBG; ++g) {
             const long long p0 = pb + 4 * kThreads * g;
             for (long long q = p0; q < p0 + 4 && q < a.npix; ++q) {
-                const unsigned c = color_px(fl[q], maxrad, rmax, fast, col);
+                bool ok = true;
+                const unsigned c = color_px<false>(fl[q], maxrad, rmax, fast, col, ok);
                 out[q * 3] = (uint8_t)c;
                 out[q * 3 + 1] = (uint8_t)(c >> 8);
                 out[q * 3 + 2] = (uint8_t)(c >> 16);
             }
         }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) k_color_px(ColorArgs a) { color_pixels(a, blockIdx.x, blockIdx.y); }
+
+// One launch per chunk of fields: the colour pass of chunk k (blocks x <
+// npx_b, its maxima computed by the previous launch) beside the max pass of
+// chunk k + 1 (the other blocks): no dependency inside the launch, so the
+// colour pass's arithmetic and the max pass's reads overlap, and chunk k's
+// flow, read by the max pass one launch earlier, is re-read from the cache.
+struct ColorStep {
+    ColorArgs px, mx;
+    int npx_b, nmx_b;  // blocks per field of each role
+    int npx_f, nmx_f;  // fields of each role (0: role absent)
+};
+
+__global__ void __launch_bounds__(kThreads) k_color_step(ColorStep c)
+{
+    const int x = blockIdx.x, f = blockIdx.y;
+    if (x < c.npx_b) {
+        if (f < c.npx_f) color_pixels(c.px, x, f);
+    } else if (f < c.nmx_f) {
+        color_max(c.mx, x - c.npx_b, c.nmx_b, f);
     }
 }
 
@@ -239,15 +323,35 @@ hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmo
     if (e != hipSuccess) return e;
     // fields per chunk: ~128 MB of flow, re-read from the Infinity Cache
     const long long fbytes = a.npix * 8;
-    const int chunk = (int)std::max<long long>(1, std::min<long long>(n, (128LL << 20) / std::max(1LL, fbytes)));
+#ifndef DIS_COLOR_CHUNK_MB
+#define DIS_COLOR_CHUNK_MB 128  // r04 A/B (32 x 1080p fields): 32 / 64 / 128 MB chunks 0.41 / 0.36-0.38 / 0.32-0.34 ms
+#endif
+    const int chunk =
+        (int)std::max<long long>(1, std::min<long long>(n, ((long long)DIS_COLOR_CHUNK_MB << 20) / std::max(1LL, fbytes)));
     const unsigned mb = (unsigned)std::min<long long>(256, (a.npix + 2LL * kThreads * 8 - 1) / (2LL * kThreads * 8));
-    for (int f0 = 0; f0 < n; f0 += chunk) {
-        const int nc = std::min(chunk, n - f0);
-        a.flow = reinterpret_cast<const float2*>(flow) + (size_t)f0 * a.npix;
-        a.bgr = bgr + (size_t)f0 * a.npix * 3;
-        a.ws = ws + (size_t)kMaxStride * f0;
-        hipLaunchKernelGGL(k_color_max, dim3(mb, nc), dim3(kThreads), 0, s, a);
-        hipLaunchKernelGGL(k_color_px, dim3(bx, nc), dim3(kThreads), 0, s, a);
+    auto chunk_args = [&](int f0) {
+        ColorArgs c = a;
+        c.flow = reinterpret_cast<const float2*>(flow) + (size_t)f0 * a.npix;
+        c.bgr = bgr + (size_t)f0 * a.npix * 3;
+        c.ws = ws + (size_t)kMaxStride * f0;
+        return c;
+    };
+    // launch j: colour pass of chunk j - 1 and max pass of chunk j
+    const int nch = (n + chunk - 1) / chunk;
+    for (int j = 0; j <= nch; ++j) {
+        ColorStep c{};
+        if (j > 0) {
+            c.px = chunk_args((j - 1) * chunk);
+            c.npx_b = (int)bx;
+            c.npx_f = std::min(chunk, n - (j - 1) * chunk);
+        }
+        if (j < nch) {
+            c.mx = chunk_args(j * chunk);
+            c.nmx_b = (int)mb;
+            c.nmx_f = std::min(chunk, n - j * chunk);
+        }
+        const dim3 grid((unsigned)(c.npx_b + c.nmx_b), (unsigned)std::max(c.npx_f, c.nmx_f));
+        hipLaunchKernelGGL(k_color_step, grid, dim3(kThreads), 0, s, c);
     }
     return hipGetLastError();
 }
