@@ -69,6 +69,9 @@
 #ifndef DIS_TAP_ADDR2
 #define DIS_TAP_ADDR2 1  // iterate_split tile path, tolerance mode: byte-offset tap bases, VGPR row step
 #endif
+#ifndef DIS_TAP_ADDR3
+#define DIS_TAP_ADDR3 1  // the same byte offsets in the exact kernel, row-group bases added per update
+#endif
 #ifndef DIS_RESET_OUT
 #define DIS_RESET_OUT 1  // iterate_split: the outlier reset applied once, after the loop, on the exiting lanes
 #endif
@@ -996,7 +999,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // literal (tolerance mode only: the exact kernel is at 128 VGPRs
                 // and spilled; with literals its loop grew 463 -> 470 VALU)
                 int g3 = 12 * TS;
-                __asm__("" : "+v"(g3));
+                if constexpr (kFma) __asm__("" : "+v"(g3));
 #endif
                 iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, (kFma ? DIS_TAP_PREFETCH_FMA : DIS_TAP_PREFETCH) != 0>(
                                                                              a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
@@ -1009,6 +1012,23 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                                                        const float *f0 = reinterpret_cast<const float*>(c0),
                                                                    *f1 = reinterpret_cast<const float*>(c0 + g3),
                                                                    *f2 = reinterpret_cast<const float*>(c0 + g3 + g3);
+                                                       return [=](int k, int c) {
+                                                           return k < 3 ? f0[k * TS + c]
+                                                                        : k < 6 ? f1[(k - 3) * TS + c] : f2[(k - 6) * TS + c];
+                                                       };
+                                                     } else if constexpr (DIS_TAP_ADDR3) {
+                                                       // exact kernel: byte offsets too, the two further row-group
+                                                       // bases added per update behind opaque copies (a literal each;
+                                                       // no VGPR held across the loop)
+                                                       typedef __attribute__((address_space(3))) const char* lds_cp;
+                                                       typedef __attribute__((address_space(3))) const float* lds_fp;
+                                                       const int tb = __mul24(cv, M4) + K4;
+                                                       lds_cp c0 = (lds_cp)tqb + (tb + xor1i(tb));
+                                                       lds_cp c1 = c0 + 12 * TS;
+                                                       lds_cp c2 = c0 + 24 * TS;
+                                                       __asm__("" : "+v"(c1));
+                                                       __asm__("" : "+v"(c2));
+                                                       const lds_fp f0 = (lds_fp)c0, f1 = (lds_fp)c1, f2 = (lds_fp)c2;
                                                        return [=](int k, int c) {
                                                            return k < 3 ? f0[k * TS + c]
                                                                         : k < 6 ? f1[(k - 3) * TS + c] : f2[(k - 6) * TS + c];
