@@ -53,43 +53,24 @@ constexpr Wheel make_wheel()
 
 __constant__ Wheel c_wheel = make_wheel();  // read-only table: scalar/constant cache loads
 
-// a / b, correctly rounded, for 2^-60 <= b <= 2^60 and a = 0 or
-// b 2^-30 <= a <= b: the core of the IEEE division sequence (reciprocal, one
-// Newton step, quotient, two remainder corrections -- v_div_scale /
-// v_div_fmas / v_div_fixup without their scaling and special cases, which
-// these operands never need: the same bits). kFast: that core, clearing `ok`
-// outside its domain; otherwise the IEEE division.
+// a / b and sqrtf(x), correctly rounded on their fast domains, through the
+// IEEE sequences' cores (dis_device.h div_core / sqrt_core); kFast: that core,
+// clearing `ok` outside its domain (the caller then recomputes the pixel the
+// IEEE way); otherwise the IEEE operation
 template <bool kFast>
 __device__ __forceinline__ float div_rn(float a, float b, bool& ok)
 {
     if constexpr (!kFast) return a / b;
-    ok = ok && b >= 0x1p-60f && b <= 0x1p60f && (a == 0.0f || (a >= b * 0x1p-30f && a <= b));
-    float y = __builtin_amdgcn_rcpf(b);
-    const float e = __builtin_fmaf(-b, y, 1.0f);
-    y = __builtin_fmaf(e, y, y);
-    float q = a * y;
-    float r = __builtin_fmaf(-b, q, a);
-    q = __builtin_fmaf(r, y, q);
-    r = __builtin_fmaf(-b, q, a);
-    return __builtin_fmaf(r, y, q);
+    ok = ok && div_core_ok(a, b);
+    return div_core(a, b);
 }
 
-// sqrtf(x), correctly rounded, for x = +0 or 2^-96 <= x <= 2^96: v_sqrt_f32
-// (within one ulp) and the residual tests of both neighbours (exact: see
-// dis_device.h sqrt_cr; no denormal scaling in this range). x here is a sum
-// of squares (never -0). kFast: that, clearing `ok` outside the range;
-// otherwise the IEEE sqrtf.
 template <bool kFast>
 __device__ __forceinline__ float sqrt_rn(float x, bool& ok)
 {
     if constexpr (!kFast) return sqrtf(x);
-    ok = ok && ((x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f);
-    const float r = __builtin_amdgcn_sqrtf(x);
-    const float rm = __int_as_float(__float_as_int(r) - 1);
-    const float rp = __int_as_float(__float_as_int(r) + 1);
-    float y = __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
-    y = __builtin_fmaf(-rp, r, x) > 0.0f ? rp : y;
-    return x == 0.0f ? x : y;
+    ok = ok && sqrt_core_ok(x);
+    return sqrt_core(x);
 }
 
 // atan2(y, x) for finite y, x: t = min/max in [0, 1], atan(t) = t + t z P(z),

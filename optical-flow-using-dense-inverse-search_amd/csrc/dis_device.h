@@ -180,4 +180,43 @@ __device__ __forceinline__ float div_pre(float a, float b, float r)
 #endif
 }
 
+// a / b, correctly rounded, for 2^-60 <= b <= 2^60 and a = 0 or
+// b 2^-30 <= a <= b (div_core_ok): the core of the IEEE division sequence the
+// compiler emits (v_rcp_f32, one Newton step, quotient, two remainder
+// corrections) without v_div_scale / v_div_fmas / v_div_fixup, whose scaling
+// and special cases these operands never need. The final step's correct
+// rounding rests on the refined reciprocal, i.e. on v_rcp_f32's accuracy:
+// tools/color_core_check (a -m gpu test) compares it with the IEEE division on
+// every divisor mantissa. Used by the colour kernel (atan2's min / max).
+__device__ __forceinline__ bool div_core_ok(float a, float b)
+{
+    return b >= 0x1p-60f && b <= 0x1p60f && (a == 0.0f || (a >= b * 0x1p-30f && a <= b));
+}
+__device__ __forceinline__ float div_core(float a, float b)
+{
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    float q = a * y;
+    float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// sqrtf(x), correctly rounded, for x = +0 or 2^-96 <= x <= 2^96 (sqrt_core_ok):
+// v_sqrt_f32 (within one ulp) and the residual tests of both neighbours (the
+// two-sided form of sqrt_cr above; no denormal scaling in this range);
+// tools/color_core_check compares it with sqrtf on whole binades.
+__device__ __forceinline__ bool sqrt_core_ok(float x) { return (x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f; }
+__device__ __forceinline__ float sqrt_core(float x)
+{
+    const float r = __builtin_amdgcn_sqrtf(x);
+    const float rm = __int_as_float(__float_as_int(r) - 1);
+    const float rp = __int_as_float(__float_as_int(r) + 1);
+    float y = __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
+    y = __builtin_fmaf(-rp, r, x) > 0.0f ? rp : y;
+    return x == 0.0f ? x : y;
+}
+
 }  // namespace dis

@@ -514,6 +514,20 @@ def test_pyramid_sqrt_is_correctly_rounded_on_every_input():
     assert out.returncode == 0 and "sqrt_cr: 0 mismatches" in out.stdout, out.stdout + out.stderr
 
 
+@pytest.mark.gpu
+def test_colour_fast_division_and_sqrt_are_ieee():
+    # dis_color.hip's fast cores (dis_device.h div_core / sqrt_core) rest on
+    # this GPU's v_rcp_f32 / v_sqrt_f32 seeds: tools/color_core_check compares
+    # them with IEEE a / b and sqrtf on every divisor mantissa and on whole
+    # binades of the sqrt domain
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "color_core_check")
+    assert os.path.exists(exe), "tools/color_core_check not built (__graft_entry__.build)"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.count("mismatches 0") == 8, out.stdout + out.stderr
+
+
 def test_medium_4k_batch_bitexact(disflow_mod, oracle):
     # BASELINE config 3 (3840x2160 MEDIUM, the LDS/HBM tiling stress case):
     # a batch of 2 (2-lanes-per-patch kernels on the big levels, 2 streams),
@@ -573,6 +587,32 @@ def test_flow_color_batch_persistent_bitexact(disflow_mod, oracle, maxmotion):
     got = disflow_mod.flow_color(f, maxmotion)
     for k in range(5):
         assert np.array_equal(got[k], oracle.flow_color(f[k], maxmotion)), f"field {k}"
+
+
+def test_flow_color_chunked_fast_paths_bitexact(disflow_mod, oracle):
+    # 9 full-HD fields = two 128 MB chunks (8 + 1): the colour pass of chunk 0 shares
+    # a launch with the max pass of chunk 1 (k_color_step). Values at the
+    # edges of the fast division / sqrt domains (dis_color.hip div_rn,
+    # sqrt_rn): axis-aligned flows (min/max quotient 0), quotients around
+    # 2^-30, squared radii around 2^-96 and 2^96 (fixed range), denormals --
+    # each either on the exact fast path or recomputed the IEEE way
+    W, H, n = 1920, 1080, 9
+    rng = np.random.default_rng(21)
+    scales = np.array([4, 0.3, 40, 1e-3, 7, 1e-20, 2, 5, 1e6], np.float32)
+    f = (rng.standard_normal((n, H, W, 2)) * scales[:, None, None, None]).astype(np.float32)
+    e = np.array([(1.0, 0.0), (0.0, -2.0), (1.0, 2.0 ** -30), (1.0, 2.0 ** -31), (3.0, 2.0 ** -29.5),
+                  (2.0 ** -48, 2.0 ** -49), (2.0 ** -49, 0.0), (2.0 ** -60, 2.0 ** -61), (1e-38, 1e-39),
+                  (2.0 ** 47, 2.0 ** 46), (-0.0, 5.0), (5.0, -0.0)], np.float32)
+    for k in range(n):
+        f[k, 7, 100:100 + len(e)] = e * (k + 1)
+    got = disflow_mod.flow_color(f, -1.0)
+    for k in range(n):
+        assert np.array_equal(got[k], oracle.flow_color(f[k], -1.0)), f"field {k}"
+    small = f[:2, :64, :64].copy()
+    for mm in (2.0 ** -50, 2.0 ** 50):  # fixed ranges putting fx*fx + fy*fy outside [2^-96, 2^96]
+        g = disflow_mod.flow_color(small, mm)
+        for k in range(2):
+            assert np.array_equal(g[k], oracle.flow_color(small[k], mm)), f"maxmotion {mm} field {k}"
 
 
 def test_flow_color_unaligned_output_bitexact(disflow_mod, oracle):
