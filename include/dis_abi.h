@@ -140,14 +140,19 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
 /* Stage dumps for parity tests: copy one intermediate of pair `pair` from the
  * last calc on this context into host memory `dst` (count floats). Stages:
  * level image frame 0 / frame 1, frame-0 Sobel dx / dy, per-patch u (n_l*2),
- * dense flow (W_l*H_l*2). Requires dis_set_debug(ctx, 1) before the calc. */
+ * dense flow (W_l*H_l*2). Requires dis_set_debug(ctx, 1) before the calc.
+ * DIS_STAGE_FALLBACK (count 1, no debug mode needed): the number of patch
+ * blocks of level `level` whose start positions were too spread for the LDS
+ * tile and were searched by the fallback kernel in the last calc, summed over
+ * the call's sub-batches (`pair` only has to lie in the last batch). */
 typedef enum dis_stage {
     DIS_STAGE_IMG0 = 0,
     DIS_STAGE_IMG1 = 1,
     DIS_STAGE_DX0 = 2,
     DIS_STAGE_DY0 = 3,
     DIS_STAGE_PATCH_U = 4,
-    DIS_STAGE_DENSE = 5
+    DIS_STAGE_DENSE = 5,
+    DIS_STAGE_FALLBACK = 6
 } dis_stage;
 dis_status dis_set_debug(dis_ctx* ctx, int enable);
 

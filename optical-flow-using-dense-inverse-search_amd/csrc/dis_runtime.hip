@@ -144,6 +144,7 @@ struct dis_ctx {
     int debug = 0;
     int variant = 0;  // 0 auto, 1 generic only, 2/3/4/5/6: patch_size-8 search with 4/2/8/1/64 lanes per patch
     int last_batch = 0;
+    int last_nsub = 1;  // sub-batches of the last calc (their fallback counters, DIS_STAGE_FALLBACK)
     hipStream_t own = nullptr;
     static constexpr int kMaxSub = 8;
     int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
@@ -775,6 +776,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     // behind a co-running sub-batch's long search launches (measured on
     // 3840x2160 SLOW, batch 2: 36.3 ms with two streams, 24.1 ms with one).
     const int S = c->p.var_refine_iters > 0 ? 1 : std::min(c->nsub, n);
+    c->last_nsub = std::max(S, 1);
     std::vector<int> stages = {kStageFront};
     for (int l = c->g.C; l >= c->g.F; --l) stages.push_back(l);
     stages.push_back(kStageBack);
@@ -1351,6 +1353,7 @@ dis_status dis_stage_size(dis_ctx* c, int stage, int level, size_t* count)
         case DIS_STAGE_DY0: *count = (size_t)L.W * L.H; return DIS_OK;
         case DIS_STAGE_PATCH_U: *count = (size_t)L.n * 2; return DIS_OK;
         case DIS_STAGE_DENSE: *count = (size_t)L.W * L.H * 2; return DIS_OK;
+        case DIS_STAGE_FALLBACK: *count = 1; return DIS_OK;
         default: return fail(DIS_ERR_INVALID_ARGUMENT, "unknown stage");
     }
 }
@@ -1369,6 +1372,15 @@ dis_status dis_debug_dump(dis_ctx* c, int stage, int level, int pair, float* dst
         return fail(DIS_ERR_INVALID_ARGUMENT, "stage not computed below finest_scale");
     DIS_HIP(hipSetDevice(c->device));
     DIS_HIP(hipDeviceSynchronize());
+    if (stage == DIS_STAGE_FALLBACK) {  // blocks the level's tile search listed for k_search8_fb, all sub-batches
+        std::vector<int> cnt((size_t)c->last_nsub);
+        for (int k = 0; k < c->last_nsub; ++k)
+            DIS_HIP(hipMemcpy(&cnt[k], c->fb + (size_t)k * dis::kMaxLevels + level, sizeof(int), hipMemcpyDeviceToHost));
+        long long t = 0;
+        for (int v : cnt) t += v;
+        *dst = (float)t;
+        return DIS_OK;
+    }
     const void* src = nullptr;
     switch (stage) {
         case DIS_STAGE_IMG0: src = c->img0 + pair * g.plane_stride + L.plane_off; break;

@@ -44,7 +44,7 @@ DIS_ERR_INTERNAL = -5
 MEM_HOST = 0
 MEM_DEVICE = 1
 
-STAGE_IMG0, STAGE_IMG1, STAGE_DX0, STAGE_DY0, STAGE_PATCH_U, STAGE_DENSE = range(6)
+STAGE_IMG0, STAGE_IMG1, STAGE_DX0, STAGE_DY0, STAGE_PATCH_U, STAGE_DENSE, STAGE_FALLBACK = range(7)
 
 PRECISION_EXACT, PRECISION_FMA = 0, 1
 
@@ -316,6 +316,11 @@ class DenseInverseSearch:
         out = np.empty(cnt.value, np.float32)
         _check(lib().dis_debug_dump(self._ctx, stage, level, pair, _ptr(out), cnt.value))
         return out
+
+    def fallback_blocks(self, level: int) -> int:
+        """Patch blocks of `level` the last calc searched with the fallback
+        kernel (start positions too spread for the LDS tile), all sub-batches."""
+        return int(self.debug_dump(STAGE_FALLBACK, level)[0])
 
     def set_kernel_timing(self, on: bool = True) -> None:
         _check(lib().dis_set_kernel_timing(self._ctx, int(on)))

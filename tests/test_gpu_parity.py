@@ -732,3 +732,30 @@ def test_paper_mode_identical_frames_zero_flow_on_gpu(disflow_mod):
     p.paper_mode = 1
     got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I0)
     assert np.array_equal(got, np.zeros_like(got))
+
+
+@pytest.mark.parametrize("seed,W,H,preset,paper", [
+    (3, 1920, 1080, "MEDIUM", 0),
+    (4, 1920, 1080, "FAST", 0),
+    (5, 1920, 1080, "ULTRAFAST", 0),
+    (6, 1920, 1080, "MEDIUM", 1),
+    (7, 3840, 2160, "MEDIUM", 0),
+])
+def test_structured_scenes_bitexact(disflow_mod, oracle, seed, W, H, preset, paper):
+    # tests/scenes.py: flat regions (zero gradients), sharp edges, objects moving
+    # independently by up to 20 px (occlusions, outlier resets, spread blocks),
+    # a border-crossing and a saturated object, sensor noise -- the statistics
+    # of real footage the value-noise pairs lack; a batch of two scenes, full size
+    import scenes
+    pairs = [scenes.scene_pair(seed * 10 + k, W, H) for k in range(2)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
+    p.paper_mode = paper
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2)
+    got = eng.calc_batch(I0, I1)
+    if seed == 3:  # the scenes send spread blocks to the fallback kernel (the unrelated-frames test aside, only here)
+        assert sum(eng.fallback_blocks(l) for l in range(p.finest_scale, p.coarsest_scale + 1)) > 0
+    with oracle.threads(16):
+        for k in range(2):
+            _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"scene {seed}/{k} {preset} paper {paper}")

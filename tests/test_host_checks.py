@@ -40,3 +40,17 @@ def test_host_code_under_asan_ubsan(tmp_path):
                          timeout=300, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failures" in out.stdout
+
+
+def test_structured_scene_generator():
+    # tests/scenes.py (the structured parity scenes): deterministic, u8, with
+    # flat regions, saturated pixels and independent object motion
+    import numpy as np
+    import scenes
+    a0, a1 = scenes.scene_pair(3, 320, 180)
+    b0, b1 = scenes.scene_pair(3, 320, 180)
+    assert a0.dtype == np.uint8 and a0.shape == (180, 320)
+    assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+    assert not np.array_equal(a0, a1)
+    # flat regions: many pixels equal to a horizontal neighbour (noise sigma 0.6 rounds to 0 often)
+    assert (a0[:, 1:] == a0[:, :-1]).mean() > 0.3
