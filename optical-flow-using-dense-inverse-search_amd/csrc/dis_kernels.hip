@@ -303,6 +303,19 @@ __global__ void __launch_bounds__(64) k_search_generic(SearchArgs a)
 // +0, weights 0.5 each (Q6, Q7: zero-initialised), then f /= w.
 // grid: (ceil(W/64), ceil(H/4), batch)
 // ---------------------------------------------------------------------------
+// RN(1 / (0.5 n)) for n covering patches (compile-time IEEE division: the
+// same bits as the division at run time)
+struct DensifyRcp {
+    float r[257];
+};
+constexpr DensifyRcp make_densify_rcp()
+{
+    DensifyRcp t{};
+    for (int n = 1; n <= 256; ++n) t.r[n] = 1.0f / (0.5f * (float)n);
+    return t;
+}
+__constant__ DensifyRcp c_densify_rcp = make_densify_rcp();
+
 __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
 {
     const int x = blockIdx.x * 64 + threadIdx.x;
@@ -310,11 +323,13 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
     const int pair = blockIdx.z;
     if (x >= a.W || y >= a.H) return;
     const int hp = a.ps / 2;
-    // patches covering x: ref.x in [x - hp + 1, x + hp]
-    int gx0 = floordiv(x - a.offw - hp + 1 + a.steps - 1, a.steps);
-    int gx1 = floordiv(x - a.offw + hp, a.steps);
-    int gy0 = floordiv(y - a.offh - hp + 1 + a.steps - 1, a.steps);
-    int gy1 = floordiv(y - a.offh + hp, a.steps);
+    // patches covering x: ref.x in [x - hp + 1, x + hp] (floor divisions through
+    // the reciprocal of the grid step: exact for |a| < 2^20, floordiv_r)
+    const float rs = __builtin_amdgcn_rcpf((float)a.steps);
+    int gx0 = floordiv_r(x - a.offw - hp + 1 + a.steps - 1, rs);
+    int gx1 = floordiv_r(x - a.offw + hp, rs);
+    int gy0 = floordiv_r(y - a.offh - hp + 1 + a.steps - 1, rs);
+    int gy1 = floordiv_r(y - a.offh + hp, rs);
     gx0 = gx0 < 0 ? 0 : gx0;
     gy0 = gy0 < 0 ? 0 : gy0;
     gx1 = gx1 > a.npw - 1 ? a.npw - 1 : gx1;
@@ -329,7 +344,10 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
             for (int gy = gy0; gy <= gy1; ++gy) {
                 const float2 v = u[gx * a.nph + gy];
                 const float d = bilinear_replicate(I1, a.W, a.H, (float)x + v.x, (float)y + v.y) - i0;
-                const float c = 1.0f / fmaxf(1.0f, fabsf(d));
+                // 1 / max(1, |d|): the IEEE division's core where it is exact
+                // (dis_device.h div_core, m in [1, 2^30]; tools/color_core_check)
+                const float m = fmaxf(1.0f, fabsf(d));
+                const float c = m <= 0x1p30f ? div_core(1.0f, m) : 1.0f / m;
                 fx = fx + c * v.x;
                 fy = fy + c * v.y;
                 w = w + c;
@@ -342,6 +360,17 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
                 fy = fy + v.y * 0.5f;
                 w = w + 0.5f;
             }
+        // w = 0.5 n exactly: fx / w correctly rounded through the tabulated
+        // RN(1 / w) (div_pre); tiny nonzero numerators, whose remainders could
+        // underflow, and more than 256 covering patches divide the IEEE way
+        const int n = (int)(w * 2.0f);
+        const bool tiny = (fx != 0.0f && fabsf(fx) < 0x1p-100f) || (fy != 0.0f && fabsf(fy) < 0x1p-100f);
+        if (n > 0 && n <= 256 && !tiny) {
+            const float r = c_densify_rcp.r[n];
+            fx = div_pre(fx, w, r);
+            fy = div_pre(fy, w, r);
+            w = 0.0f;  // done
+        }
     }
     if (w > 0) {
         fx = fx / w;
