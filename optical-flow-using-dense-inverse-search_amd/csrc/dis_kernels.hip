@@ -316,25 +316,39 @@ constexpr DensifyRcp make_densify_rcp()
 }
 __constant__ DensifyRcp c_densify_rcp = make_densify_rcp();
 
-__global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
+// block: kDenBX x kDenBY pixels; the patches covering it (at most
+// ((kDenBX + 16) / 1 + 1) x ((kDenBY + 16) / 1 + 1) for ps <= 16, step >= 1)
+// staged in LDS once, read by every pixel from there (the x-major patch array
+// read straight per pixel cost 32 cache lines per wave-load: 344 us per 4K
+// level-0 pair of planes, L1/L2-bound)
+constexpr int kDenBX = 32, kDenBY = 8;
+constexpr int kDenPX = kDenBX + 17, kDenPY = kDenBY + 17;
+
+__global__ void __launch_bounds__(kDenBX * kDenBY) k_densify(DensifyArgs a)
 {
-    const int x = blockIdx.x * 64 + threadIdx.x;
-    const int y = blockIdx.y * 4 + threadIdx.y;
+    __shared__ float2 su[kDenPX * kDenPY];
+    const int x0 = blockIdx.x * kDenBX, y0 = blockIdx.y * kDenBY;
+    const int x = x0 + threadIdx.x;
+    const int y = y0 + threadIdx.y;
     const int pair = blockIdx.z;
-    if (x >= a.W || y >= a.H) return;
     const int hp = a.ps / 2;
     // patches covering x: ref.x in [x - hp + 1, x + hp] (floor divisions through
     // the reciprocal of the grid step: exact for |a| < 2^20, floordiv_r)
     const float rs = __builtin_amdgcn_rcpf((float)a.steps);
-    int gx0 = floordiv_r(x - a.offw - hp + 1 + a.steps - 1, rs);
-    int gx1 = floordiv_r(x - a.offw + hp, rs);
-    int gy0 = floordiv_r(y - a.offh - hp + 1 + a.steps - 1, rs);
-    int gy1 = floordiv_r(y - a.offh + hp, rs);
-    gx0 = gx0 < 0 ? 0 : gx0;
-    gy0 = gy0 < 0 ? 0 : gy0;
-    gx1 = gx1 > a.npw - 1 ? a.npw - 1 : gx1;
-    gy1 = gy1 > a.nph - 1 ? a.nph - 1 : gy1;
+    auto lo = [&](int v, int off) { return max(0, floordiv_r(v - off - hp + 1 + a.steps - 1, rs)); };
+    auto hi = [&](int v, int off, int n) { return min(n - 1, floordiv_r(v - off + hp, rs)); };
+    const int bx0 = lo(x0, a.offw), by0 = lo(y0, a.offh);
+    const int bnx = hi(min(x0 + kDenBX - 1, a.W - 1), a.offw, a.npw) - bx0 + 1;
+    const int bny = hi(min(y0 + kDenBY - 1, a.H - 1), a.offh, a.nph) - by0 + 1;
     const float2* u = a.u + (size_t)pair * a.u_stride;
+    for (int k = threadIdx.y * kDenBX + threadIdx.x; k < bnx * bny; k += kDenBX * kDenBY) {
+        const int cx = k / bny, cy = k - cx * bny;  // consecutive threads: consecutive patch ids
+        su[cx * bny + cy] = u[(bx0 + cx) * a.nph + by0 + cy];
+    }
+    __syncthreads();
+    if (x >= a.W || y >= a.H) return;
+    const int gx0 = lo(x, a.offw), gx1 = hi(x, a.offw, a.npw);
+    const int gy0 = lo(y, a.offh), gy1 = hi(y, a.offh, a.nph);
     float fx = 0.0f, fy = 0.0f, w = 0.0f;
     if (a.paper) {  // SURVEY 8f row 4 (oracle densify_paper)
         const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
@@ -342,7 +356,7 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
         const float i0 = I0[(size_t)y * a.W + x];
         for (int gx = gx0; gx <= gx1; ++gx)
             for (int gy = gy0; gy <= gy1; ++gy) {
-                const float2 v = u[gx * a.nph + gy];
+                const float2 v = su[(gx - bx0) * bny + gy - by0];
                 const float d = bilinear_replicate(I1, a.W, a.H, (float)x + v.x, (float)y + v.y) - i0;
                 // 1 / max(1, |d|): the IEEE division's core where it is exact
                 // (dis_device.h div_core, m in [1, 2^30]; tools/color_core_check)
@@ -355,7 +369,7 @@ __global__ void __launch_bounds__(256) k_densify(DensifyArgs a)
     } else {
         for (int gx = gx0; gx <= gx1; ++gx)
             for (int gy = gy0; gy <= gy1; ++gy) {
-                const float2 v = u[gx * a.nph + gy];
+                const float2 v = su[(gx - bx0) * bny + gy - by0];
                 fx = fx + v.x * 0.5f;
                 fy = fy + v.y * 0.5f;
                 w = w + 0.5f;
@@ -550,7 +564,9 @@ hipError_t launch_paper_init(const PaperInitArgs& a, int batch, hipStream_t s)
 
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_densify, grid2d(a.W, a.H, batch), dim3(64, 4), 0, s, a);
+    if (a.ps > 16 || a.steps < 1) return hipErrorInvalidValue;  // the staged patch block (kDenPX x kDenPY)
+    hipLaunchKernelGGL(k_densify, dim3((a.W + kDenBX - 1) / kDenBX, (a.H + kDenBY - 1) / kDenBY, batch),
+                       dim3(kDenBX, kDenBY), 0, s, a);
     return hipGetLastError();
 }
 
