@@ -204,6 +204,16 @@ __device__ __forceinline__ float div_core(float a, float b)
     return __builtin_fmaf(r, y, q);
 }
 
+// 1 / max(1, |d|), correctly rounded (the paper mode's vote weight, Kroeger et
+// al. 2016 eq. 4): the division core for m = max(1, |d|) <= 2^30 (numerator 1
+// within [m 2^-30, m]), the IEEE division above that (and for NaN-free
+// infinities)
+__device__ __forceinline__ float recip_max1(float d)
+{
+    const float m = fmaxf(1.0f, fabsf(d));
+    return m <= 0x1p30f ? div_core(1.0f, m) : 1.0f / m;
+}
+
 // sqrtf(x), correctly rounded, for x = +0 or 2^-96 <= x <= 2^96 (sqrt_core_ok):
 // v_sqrt_f32 (within one ulp) and the residual tests of both neighbours (the
 // two-sided form of sqrt_cr above; no denormal scaling in this range);

@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                         const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
                         const float d =
                             bilinear_replicate(I1, a.wF, a.hF, (float)xg + t.x, (float)yg + t.y) - i0v;
-                        const float cw = 1.0f / fmaxf(1.0f, fabsf(d));
+                        const float cw = recip_max1(d);  // correctly rounded (dis_device.h)
                         fx = fx + cw * t.x;
                         fy = fy + cw * t.y;
                         w = w + cw;

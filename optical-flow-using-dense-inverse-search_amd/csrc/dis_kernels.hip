@@ -358,10 +358,7 @@ __global__ void __launch_bounds__(kDenBX * kDenBY) k_densify(DensifyArgs a)
             for (int gy = gy0; gy <= gy1; ++gy) {
                 const float2 v = su[(gx - bx0) * bny + gy - by0];
                 const float d = bilinear_replicate(I1, a.W, a.H, (float)x + v.x, (float)y + v.y) - i0;
-                // 1 / max(1, |d|): the IEEE division's core where it is exact
-                // (dis_device.h div_core, m in [1, 2^30]; tools/color_core_check)
-                const float m = fmaxf(1.0f, fabsf(d));
-                const float c = m <= 0x1p30f ? div_core(1.0f, m) : 1.0f / m;
+                const float c = recip_max1(d);  // 1 / max(1, |d|), correctly rounded (dis_device.h)
                 fx = fx + c * v.x;
                 fy = fy + c * v.y;
                 w = w + c;
@@ -529,8 +526,9 @@ __global__ void __launch_bounds__(256) k_paper_init(PaperInitArgs a)
     const int id = gx * a.nph + gy;
     const int x = (gx * a.steps + a.offw) >> 1, y = (gy * a.steps + a.offh) >> 1;  // level l+1 pixel
     const int st = a.steps, hp = a.hp;
-    int cx0 = floordiv(x - a.c_offw - hp + st, st), cx1 = floordiv(x - a.c_offw + hp, st);
-    int cy0 = floordiv(y - a.c_offh - hp + st, st), cy1 = floordiv(y - a.c_offh + hp, st);
+    const float rst = __builtin_amdgcn_rcpf((float)st);  // floordiv_r: exact for |a| < 2^20
+    int cx0 = floordiv_r(x - a.c_offw - hp + st, rst), cx1 = floordiv_r(x - a.c_offw + hp, rst);
+    int cy0 = floordiv_r(y - a.c_offh - hp + st, rst), cy1 = floordiv_r(y - a.c_offh + hp, rst);
     cx0 = max(cx0, 0);
     cy0 = max(cy0, 0);
     cx1 = min(cx1, a.c_npw - 1);
@@ -544,7 +542,7 @@ __global__ void __launch_bounds__(256) k_paper_init(PaperInitArgs a)
         for (int cy = cy0; cy <= cy1; ++cy) {
             const float2 v = u[cx * a.c_nph + cy];
             const float d = bilinear_replicate(I1, a.c_W, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
-            const float c = 1.0f / fmaxf(1.0f, fabsf(d));
+            const float c = recip_max1(d);  // 1 / max(1, |d|), correctly rounded (dis_device.h)
             fx = fx + c * v.x;
             fy = fy + c * v.y;
             w = w + c;
