@@ -508,7 +508,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
             if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
-            if (fast) DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (g.C + 1), s));
+            // (zeroed on every path: DIS_STAGE_FALLBACK reports them after any calc)
+            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (g.C + 1), s));
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
             for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }

@@ -417,8 +417,14 @@ def test_uncorrelated_frames_exercise_tile_fallback(disflow_mod, oracle):
     I1 = np.ascontiguousarray(I1[::-1, ::-1])
     p = disflow_mod.Params(coarsest_scale=5, finest_scale=0, patch_size=8, iterations=10,
                            patch_overlap=0.625, patch_normalization=1)
-    got = disflow_mod.DenseInverseSearch(p, W, H).calc(I0, I1)
+    eng = disflow_mod.DenseInverseSearch(p, W, H)
+    got = eng.calc(I0, I1)
     _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "flow")
+    listed = [eng.fallback_blocks(l) for l in range(p.finest_scale, p.coarsest_scale + 1)]
+    assert sum(listed) > 0, listed  # the fallback kernel did run (DIS_STAGE_FALLBACK)
+    eng.set_variant(1)  # generic kernels: no tile / fallback split, the counters read 0
+    eng.calc(I0, I1)
+    assert all(eng.fallback_blocks(l) == 0 for l in range(p.finest_scale, p.coarsest_scale + 1))
 
 
 def test_dense_grid_overlap_fallbacks(disflow_mod, oracle):
