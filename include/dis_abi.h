@@ -170,8 +170,11 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * with one launch per coarse level (what 0 does in the default build), 8 =
  * auto with the coarse levels at 8 lanes per patch fused into one launch
  * (k_search8_head, ABI v6; measured 0.6-1.0 % slower per step, so not the
- * default). All are bit-identical; the switch exists for parity tests and A/B
- * timing. */
+ * default), 9 = 2 lanes per patch on every level with the usable LDS tile
+ * capped at 24 rows / columns, so that most patch blocks take the fallback
+ * list and kernel (a parity-test switch: natural inputs rarely spread a
+ * block's start positions beyond the full tile). All are bit-identical; the
+ * switch exists for parity tests and A/B timing. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 
 /* Arithmetic of the patch_size-8 search kernels (ABI v4; no reference

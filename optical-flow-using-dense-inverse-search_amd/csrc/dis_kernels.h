@@ -61,6 +61,8 @@ struct Search8Args {
     int lanes_per_patch;      // 1, 2, 4 or 8 (k_search8<LPP>)
     const float2* dense_coarse;  // non-null: init from the coarser level's DENSE flow (variational
     long long dense_stride;      //   refinement on) instead of u_coarse; float2 per pair
+    int tile_cap;             // > 0: usable tile rows / columns capped at this (variant 9, a parity-test
+                              //   switch that sends most blocks through the fallback list); 0 = the full tile
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline

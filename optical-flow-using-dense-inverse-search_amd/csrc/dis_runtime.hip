@@ -117,7 +117,7 @@ static int search8_lanes(int variant, long long patches, int steps)
 {
     const int big = (DIS_LPP_BIG == 1 && !dis::search8_lpp1_fits(steps)) ? 2 : DIS_LPP_BIG;
     if (variant == 2) return 4;
-    if (variant == 3) return 2;
+    if (variant == 3 || variant == 9) return 2;
     if (variant == 4) return 8;
     if (variant == 5) return dis::search8_lpp1_fits(steps) ? 1 : 2;
     if (variant == 6) return 64;  // one wave per patch (exact, non-paper levels)
@@ -547,6 +547,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         b.lanes_per_patch = search8_lanes(c->variant, (long long)Lq.npw * Lq.nph * n, Lq.steps);
         b.tile_stride = dis::search8_tile_stride(Lq.steps, b.lanes_per_patch);
         b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(Lq.steps, b.lanes_per_patch) : 0;
+        b.tile_cap = c->variant == 9 ? 24 : 0;  // variant 9: most blocks through the fallback list
         b.fb_count = fb_count + lq;
         b.fb_list = c->fb + c->fb_list_off[sub][lq];
         b.paper = paper ? 1 : 0;
@@ -1336,7 +1337,7 @@ dis_status dis_set_precision(dis_ctx* c, int mode)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 8) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..8");
+    if (variant < 0 || variant > 9) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..9");
     c->variant = variant;
     return DIS_OK;
 }

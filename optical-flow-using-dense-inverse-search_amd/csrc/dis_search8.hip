@@ -951,7 +951,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const bool any_valid = bnd[0] != 0x7fffffff;
     const int tx0 = bnd[0] - 10, ty0 = bnd[1] - 10;
     const int tw = bnd[2] + 10 - tx0 + 1, th = bnd[3] + 10 - ty0 + 1;
-    const bool use_tile = any_valid && tw <= kTileW<LPP> && th <= kTileH;
+    const int capw = a.tile_cap > 0 ? min(a.tile_cap, kTileW<LPP>) : kTileW<LPP>;
+    const int caph = a.tile_cap > 0 ? min(a.tile_cap, kTileH) : kTileH;
+    const bool use_tile = any_valid && tw <= capw && th <= caph;
     const int TS = TSC ? TSC : a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
 
     float u0 = ix, u1 = iy;

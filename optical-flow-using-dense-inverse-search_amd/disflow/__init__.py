@@ -291,7 +291,9 @@ class DenseInverseSearch:
         """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels,
         fused coarse head), 1 = generic only, 2 / 3 / 4 / 5 = 4 / 2 / 8 / 1 lanes per
         patch, 6 = one wave per patch, 7 = auto with one launch per coarse level (the
-        default's form), 8 = auto with the coarse levels fused into one launch."""
+        default's form), 8 = auto with the coarse levels fused into one launch, 9 = 2
+        lanes per patch with the usable LDS tile capped at 24 pixels (test hook: most
+        blocks take the fallback list and k_search8_fb)."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
 
     def set_concurrency(self, streams: int) -> None:

@@ -417,14 +417,23 @@ def test_uncorrelated_frames_exercise_tile_fallback(disflow_mod, oracle):
     I1 = np.ascontiguousarray(I1[::-1, ::-1])
     p = disflow_mod.Params(coarsest_scale=5, finest_scale=0, patch_size=8, iterations=10,
                            patch_overlap=0.625, patch_normalization=1)
+    exp = oracle.calc_from_params(I0, I1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    got = eng.calc(I0, I1)
-    _assert_bitexact(got, oracle.calc_from_params(I0, I1, p), "flow")
-    listed = [eng.fallback_blocks(l) for l in range(p.finest_scale, p.coarsest_scale + 1)]
-    assert sum(listed) > 0, listed  # the fallback kernel did run (DIS_STAGE_FALLBACK)
+    # auto: these levels are small enough for 8 lanes per patch, whose kernel
+    # reads spread blocks through L1/L2 inline; 2 lanes per patch everywhere
+    # (variant 3): the tile kernel lists blocks too spread for its LDS tile
+    # (none here: the densified initialisation is smooth) and k_search8_fb
+    # searches them; variant 9 caps the usable tile so that most blocks go
+    # through that list and kernel
+    levels = range(p.finest_scale, p.coarsest_scale + 1)
+    for variant in (0, 3, 9):
+        eng.set_variant(variant)
+        _assert_bitexact(eng.calc(I0, I1), exp, f"flow variant {variant}")
+        listed = [eng.fallback_blocks(l) for l in levels]
+        assert (sum(listed) > 0) == (variant == 9), listed  # DIS_STAGE_FALLBACK: the fallback kernel ran
     eng.set_variant(1)  # generic kernels: no tile / fallback split, the counters read 0
     eng.calc(I0, I1)
-    assert all(eng.fallback_blocks(l) == 0 for l in range(p.finest_scale, p.coarsest_scale + 1))
+    assert all(eng.fallback_blocks(l) == 0 for l in levels)
 
 
 def test_dense_grid_overlap_fallbacks(disflow_mod, oracle):
@@ -765,3 +774,32 @@ def test_structured_scenes_bitexact(disflow_mod, oracle, seed, W, H, preset, pap
     with oracle.threads(16):
         for k in range(2):
             _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"scene {seed}/{k} {preset} paper {paper}")
+
+
+@pytest.mark.parametrize("fma", [0, 1])
+def test_fallback_kernel_full_size(disflow_mod, oracle, fma):
+    # variant 9 (usable LDS tile capped at 24 rows / columns): most blocks of
+    # every level of a 1080p MEDIUM batch take the fallback list and
+    # k_search8_fb's global-read path, in both sub-batch streams -- bit-exact
+    # against the oracle and the default kernels (exact), and against the
+    # tile kernel at 2 lanes per patch everywhere (variant 3; tolerance mode,
+    # whose 8-lane coarse-level kernels sum in another order)
+    W, H = 1920, 1080
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    pairs = [disflow_mod.synth_pair(700 + k, W, H) for k in range(2)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2)
+    eng.set_precision(fma)
+    eng.set_variant(3 if fma else 0)
+    ref = eng.calc_batch(I0, I1)
+    eng.set_variant(9)
+    got = eng.calc_batch(I0, I1)
+    listed = sum(eng.fallback_blocks(l) for l in range(p.finest_scale, p.coarsest_scale + 1))
+    nblocks = 2 * sum(((W >> l) // 3 // 8 + 1) * ((H >> l) // 3 // 8 + 1) for l in range(p.finest_scale, 4))
+    assert listed > nblocks // 4, (listed, nblocks)
+    for k in range(2):
+        _assert_bitexact(got[k], ref[k], f"variant 9 vs {3 if fma else 0}, pair {k}, fma {fma}")
+        if not fma:
+            with oracle.threads(16):
+                _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"variant 9 pair {k}")
