@@ -352,7 +352,7 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     constexpr int T0 = 1 << LEVELS;
     const int tid = threadIdx.x;
     if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
-        if (tid < a.nzero) a.zero[tid] = 0;
+        for (int i = tid; i < a.nzero; i += blockDim.x) a.zero[i] = 0;
         for (int i = tid; i < a.nzero2; i += blockDim.x) a.zero2[i] = 0;
     }
     // XCD-aware tile order: the dispatcher deals linear block ids round-robin

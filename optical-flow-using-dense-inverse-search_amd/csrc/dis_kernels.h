@@ -45,6 +45,16 @@ struct SearchArgs {
 
 // Fast patch-size-8 search (dis_search8.hip): gradients fused from the level
 // image, init fused from the coarser level's patch displacements.
+#ifndef DIS_FB_MERGED
+#define DIS_FB_MERGED 0  // LPP 2 levels: fallback workers inside the search launch (no k_search8_fb)
+#endif
+#ifndef DIS_FB_SPREAD
+#define DIS_FB_SPREAD 1
+#endif
+// verdict counters of the in-launch fallback workers (Search8Args::fb_decided):
+// one per XCD, on separate 128-byte lines
+constexpr int kFbSlots = DIS_FB_SPREAD ? 8 : 1, kFbSlotStride = DIS_FB_SPREAD ? 32 : 1;
+
 struct Search8Args {
     const float* img0;        // frame-0 level planes (stack)
     const float* img1;        // frame-1 level planes (stack)
@@ -66,6 +76,10 @@ struct Search8Args {
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline
+    int* fb_decided;          // non-null (LPP 2): the list is searched by fb_wgs workgroups appended
+                              //   (kFbSlots counters kFbSlotStride ints apart: workgroup id mod 8)
+    int fb_wgs;               //   to the launch (1-D grid), which start once all blocks counted
+                              //   their verdict here (zeroed before the launch); no k_search8_fb
     int paper;                // template-subtracted residual (k_search8<.., kPaper>)
     const float2* u_init;     // non-null (paper mode): per-patch initial u from k_paper_init, patch-id
     long long init_stride;    //   order, float2 per pair

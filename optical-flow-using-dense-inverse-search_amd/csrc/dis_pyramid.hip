@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_e
     const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
     const int pair = bz >> 1, frame = bz & 1;
     if (bx == 0 && yb == 0 && bz == 0) {
-        if (lane < a.nzero) a.zero[lane] = 0;
+        for (int i = lane; i < a.nzero; i += 64) a.zero[i] = 0;
         for (int i = lane; i < a.nzero2; i += 64) a.zero2[i] = 0;
     }
 #ifdef DIS_STAMP
@@ -454,7 +454,7 @@ bool pyramid2_fits(const PyramidArgs& a)
 
 hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timing t)
 {
-    if (!pyramid2_fits(a) || a.nzero > 64 || (a.nzero2 > 0 && !a.zero2)) return hipErrorInvalidValue;
+    if (!pyramid2_fits(a) || (a.nzero2 > 0 && !a.zero2)) return hipErrorInvalidValue;
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
     const int nrw = (H2 + kPyrRW - 1) / kPyrRW;  // waves per column

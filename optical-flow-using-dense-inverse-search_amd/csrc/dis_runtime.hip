@@ -126,6 +126,8 @@ static int search8_lanes(int variant, long long patches, int steps)
     return big;
 }
 
+// per sub-batch: the levels' fallback list counts, then their verdict counters
+constexpr size_t kFbCounters = dis::kMaxLevels * (1 + dis::kFbSlots * dis::kFbSlotStride);
 #ifndef DIS_PYR2
 #define DIS_PYR2 1  // the two-kernel streaming pyramid (dis_pyramid.hip) where it fits
 #endif
@@ -455,7 +457,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
                      size_t pair_stride, float2* flow, hipStream_t s, int stage, hipEvent_t wait_pyr = nullptr,
                      hipEvent_t pyr_done = nullptr, bool capturing = false)
 {
-    int* const fb_count = c->fb + (size_t)sub * dis::kMaxLevels;  // this sub-batch's fallback counts
+    // this sub-batch's fallback counts, then its verdict counts (k_search8's fallback workers)
+    int* const fb_count = c->fb + (size_t)sub * kFbCounters;
     const dis::Geometry& g = c->g;
     // this sub-batch's slice of the workspace (pairs p0 .. p0+n-1)
     float* const img0 = c->img0 + (size_t)p0 * g.plane_stride;
@@ -487,7 +490,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.levels = std::min(g.C, 6);
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
             pa.zero = fb_count;
-            pa.nzero = g.C + 1;
+            pa.nzero = dis::kMaxLevels + (g.C + 1) * dis::kFbSlots * dis::kFbSlotStride;
             if (head_lo(c, n) <= g.C) {  // the fused head's counters of this sub-batch
                 pa.zero2 = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
                 pa.nzero2 = (g.C + 1 - head_lo(c, n)) * n;
@@ -509,7 +512,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
             // (zeroed on every path: DIS_STAGE_FALLBACK reports them after any calc)
-            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (g.C + 1), s));
+            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (dis::kMaxLevels + (g.C + 1) * dis::kFbSlots * dis::kFbSlotStride), s));
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
             for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }
@@ -550,6 +553,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         b.tile_cap = c->variant == 9 ? 24 : 0;  // variant 9: most blocks through the fallback list
         b.fb_count = fb_count + lq;
         b.fb_list = c->fb + c->fb_list_off[sub][lq];
+        if (DIS_FB_MERGED && b.lanes_per_patch == 2) b.fb_decided = fb_count + dis::kMaxLevels + lq * dis::kFbSlots * dis::kFbSlotStride;
         b.paper = paper ? 1 : 0;
         b.iters = g.iters;
         b.norm = g.norm;
@@ -1188,14 +1192,14 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess;
     if (ok) {
-        size_t off = (size_t)dis_ctx::kMaxSub * dis::kMaxLevels;
+        size_t off = (size_t)dis_ctx::kMaxSub * kFbCounters;
         for (int k = 0; k < dis_ctx::kMaxSub; ++k)
             for (int l = 0; l <= g.C; ++l) {
                 c->fb_list_off[k][l] = off;
                 off += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8) * B;  // 8x8 blocks (the most)
             }
         ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
-             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * dis::kMaxLevels) == hipSuccess &&
+             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * kFbCounters) == hipSuccess &&
              hipMalloc(&c->head_done, sizeof(int) * dis_ctx::kMaxSub * dis::kHeadMax * B) == hipSuccess;
     }
 #ifdef DIS_STAMP  // diagnostic builds: per-call clocks of each sub-batch stream (tools/stamp_probe.py)
@@ -1377,7 +1381,7 @@ dis_status dis_debug_dump(dis_ctx* c, int stage, int level, int pair, float* dst
     if (stage == DIS_STAGE_FALLBACK) {  // blocks the level's tile search listed for k_search8_fb, all sub-batches
         std::vector<int> cnt((size_t)c->last_nsub);
         for (int k = 0; k < c->last_nsub; ++k)
-            DIS_HIP(hipMemcpy(&cnt[k], c->fb + (size_t)k * dis::kMaxLevels + level, sizeof(int), hipMemcpyDeviceToHost));
+            DIS_HIP(hipMemcpy(&cnt[k], c->fb + (size_t)k * kFbCounters + level, sizeof(int), hipMemcpyDeviceToHost));
         long long t = 0;
         for (int v : cnt) t += v;
         *dst = (float)t;

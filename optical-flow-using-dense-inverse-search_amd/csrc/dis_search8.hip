@@ -116,6 +116,9 @@ template <int LPP>
 constexpr int kCuMax = LPP == 1 ? 192 : 144;  // staged coarse patches (<= 16 x 12 / 12 x 12 for steps >= 1)
 template <int LPP>
 constexpr int kCuPer = (kCuMax<LPP> + kThreads<LPP> - 1) / kThreads<LPP>;  // coarse patches per thread
+#ifndef DIS_FB_MERGED_WGS
+#define DIS_FB_MERGED_WGS 256  // fallback workers appended to a merged launch
+#endif
 #ifndef DIS_FB_WGS
 #define DIS_FB_WGS 256
 #endif
@@ -955,6 +958,22 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int caph = a.tile_cap > 0 ? min(a.tile_cap, kTileH) : kTileH;
     const bool use_tile = any_valid && tw <= capw && th <= caph;
     const int TS = TSC ? TSC : a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
+    if constexpr (DIS_FB_MERGED && LPP == 2 && !kFallback && !kPhys) {
+        // fallback workers in this launch (k_search8, a.fb_decided): list the
+        // block if it is too spread, then count this block's verdict. The entry
+        // is an agent-scope store acknowledged before the count (the workers may
+        // run on another XCD, whose L2 does not see this one's)
+        if (a.fb_decided && tid == 0) {
+            if (!use_tile && any_valid) {
+                const int slot = atomicAdd(a.fb_count, 1);
+                __hip_atomic_store(a.fb_list + slot, (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __hip_atomic_fetch_add(a.fb_decided + ((int)blockIdx.x % kFbSlots) * kFbSlotStride, 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 
     float u0 = ix, u1 = iy;
     float uv = q ? iy : ix;  // split iteration: the lane's coordinate
@@ -1089,8 +1108,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             });
         }
     } else if (any_valid) {
-        // too spread for the tile: k_search8_fb redoes this block
-        if (tid == 0) {
+        // too spread for the tile: k_search8_fb (or this launch's fallback
+        // workers, listed above) redoes this block
+        if (tid == 0 && !a.fb_decided) {
             const int slot = atomicAdd(a.fb_count, 1);
             a.fb_list[slot] = (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi;
         }
@@ -1255,6 +1275,47 @@ __global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
+    if constexpr (DIS_FB_MERGED && LPP == 2 && !kFallback && !kPhys) {
+        if (a.fb_decided) {
+            // 1-D grid: the level's blocks (XCD-remapped as below), then
+            // a.fb_wgs fallback workers. Workgroups are dispatched in id order,
+            // so every block workgroup is resident or done before a worker
+            // starts waiting for the verdict count; none of them waits on
+            // anything, so the count completes (the wait is bounded all the same)
+            const int nbx = (a.npw + kBX<LPP> - 1) / kBX<LPP>, nby = (a.nph + kBY - 1) / kBY;
+            const int nb = (int)gridDim.x - a.fb_wgs, lin = blockIdx.x;
+            if (lin >= nb) {
+                if (threadIdx.x == 0)
+                    for (int spin = 0; spin < (1 << 22); ++spin) {  // ~0.5 us per poll, at most ~2 s
+                        int sum = 0;
+#pragma unroll
+                        for (int k = 0; k < kFbSlots; ++k)
+                            sum += __hip_atomic_load(a.fb_decided + k * kFbSlotStride, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        if (sum >= nb) break;
+                        __builtin_amdgcn_s_sleep(16);
+                    }
+                __syncthreads();
+                const int n = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a.fb_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                for (int i = lin - nb; i < n; i += a.fb_wgs) {
+                    const int e = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(a.fb_list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    const int bx = e % nbx, t = e / nbx;
+                    search_block<LPP, true, kPaper, kFma>(a, bx, t % nby, t / nby, S);
+                    __syncthreads();  // LDS reuse by the next listed block
+                }
+                return;
+            }
+            const int per = nb / 8;
+            const int t = DIS_XCD_REMAP && lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
+            const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
+            const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
+            const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
+            search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, bx, by, bz, S);
+            return;
+        }
+    }
 #if DIS_XCD_REMAP
     // XCD-aware block order: the dispatcher deals linear workgroup ids
     // round-robin to the 8 XCDs; remap so each XCD walks a contiguous run of
@@ -1425,7 +1486,15 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
             DIS_LAUNCH(t, (k_search8<1, true, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
         }
     } else if (L == 2) {
-        if (split) {
+        if (DIS_FB_MERGED && split && a.fb_decided) {  // the fallback workers appended to the launch (1-D grid)
+            Search8Args m = a;
+            m.fb_wgs = std::min<int>(DIS_FB_MERGED_WGS, (int)fb_grid.x);
+            const dim3 g1((unsigned)((long long)grid.x * grid.y * grid.z + m.fb_wgs));
+            if constexpr (!kPaper)
+                launch_ts<2, false, kPaper, kFma>(m, g1, s, t);
+            else
+                DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), g1, dim3(kThreads<2>), 0, s, m);
+        } else if (split) {
             if constexpr (!kPaper)
                 launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             else
@@ -1508,6 +1577,7 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     // in place through a non-inlined call instead made every wave of the tile
     // kernel carry a scratch frame: finest launch 940 -> 1346 us; r03.)
     const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
+    if (a.fb_decided && (!DIS_FB_MERGED || L != 2 || !split || a.gdx_plane)) return hipErrorInvalidValue;
     // persistent fallback workgroups (grid-stride over the list), one per CU
     const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
     if (a.gdx_plane) {  // physical planes (compat): exact, non-paper, LPP 2 or 8
