@@ -128,6 +128,11 @@ static int search8_lanes(int variant, long long patches, int steps)
 
 // per sub-batch: the levels' fallback list counts, then their verdict counters
 constexpr size_t kFbCounters = dis::kMaxLevels * (1 + dis::kFbSlots * dis::kFbSlotStride);
+// the counters a call zeroes (levels 0..C; the verdict counters only when merged)
+constexpr int kFbZero(int C)
+{
+    return DIS_FB_MERGED ? dis::kMaxLevels + (C + 1) * dis::kFbSlots * dis::kFbSlotStride : C + 1;
+}
 #ifndef DIS_PYR2
 #define DIS_PYR2 1  // the two-kernel streaming pyramid (dis_pyramid.hip) where it fits
 #endif
@@ -490,7 +495,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.levels = std::min(g.C, 6);
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
             pa.zero = fb_count;
-            pa.nzero = dis::kMaxLevels + (g.C + 1) * dis::kFbSlots * dis::kFbSlotStride;
+            pa.nzero = kFbZero(g.C);
             if (head_lo(c, n) <= g.C) {  // the fused head's counters of this sub-batch
                 pa.zero2 = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
                 pa.nzero2 = (g.C + 1 - head_lo(c, n)) * n;
@@ -512,7 +517,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
             // (zeroed on every path: DIS_STAGE_FALLBACK reports them after any calc)
-            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (dis::kMaxLevels + (g.C + 1) * dis::kFbSlots * dis::kFbSlotStride), s));
+            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * kFbZero(g.C), s));
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
             for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }
