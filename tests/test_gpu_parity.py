@@ -716,11 +716,13 @@ def test_paper_mode_bitexact(disflow_mod, oracle, W, H, cfg):
     exp = oracle.calc_from_params(I0, I1, p)
     exp_fb = oracle.calc_from_params(J0, I1, p)  # unrelated frames: tile fallback blocks
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    variants = ((0, "auto"), (1, "generic"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1")) \
-        if p.patch_size == 8 else ((0, "auto"),)
+    variants = ((0, "auto"), (1, "generic"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"),
+                (9, "LPP2, most blocks through the fallback list")) if p.patch_size == 8 else ((0, "auto"),)
     for variant, name in variants:
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"paper {name}")
+        if variant == 9:  # the paper-mode fallback kernel (k_search8_fb<2, kPaper>) ran
+            assert sum(eng.fallback_blocks(l) for l in range(p.finest_scale, p.coarsest_scale + 1)) > 0
         _assert_bitexact(eng.calc(J0, I1), exp_fb, f"paper {name} fallback")
 
 
