@@ -210,8 +210,9 @@ struct dis_ctx {
     float* vr_ws = nullptr;  // variational refinement workspace (kVarRefPlanes planes per pair)
     long long vr_plane = 0;
     // patch-search fallback lists (dis_search8.hip k_search8_fb): per sub-batch
-    // k, kMaxLevels counts at fb + k * kMaxLevels, then per (k, level) a list
-    // of up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
+    // k, kFbCounters counters at fb + k * kFbCounters (the levels' list counts,
+    // then the merged build's verdict counters), then per (k, level) a list of
+    // up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
     int* fb = nullptr;
     size_t fb_list_off[8][dis::kMaxLevels] = {};
     // fused coarse head (k_search8_head): per sub-batch kHeadMax x max_batch
