@@ -116,6 +116,13 @@ template <int LPP>
 constexpr int kCuMax = LPP == 1 ? 192 : 144;  // staged coarse patches (<= 16 x 12 / 12 x 12 for steps >= 1)
 template <int LPP>
 constexpr int kCuPer = (kCuMax<LPP> + kThreads<LPP> - 1) / kThreads<LPP>;  // coarse patches per thread
+#ifndef DIS_FB_LPP8
+// 1: exact modes search the LPP-2 lists at 8 lanes per patch (no spill; 2.3x
+// faster when most blocks are listed, variant 9) -- off: its 8-wave workgroups
+// wait for slots beside the other sub-batch's search, and the usually empty
+// launch then costs the step 1 % (r04 A/B)
+#define DIS_FB_LPP8 0
+#endif
 #ifndef DIS_FB_MERGED_WGS
 #define DIS_FB_MERGED_WGS 256  // fallback workers appended to a merged launch
 #endif
@@ -1376,18 +1383,21 @@ k_search8_head(HeadArgs h)
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
 // its workgroups cannot take the slots another stream's search kernel frees,
 // and the (usually empty) launch waited 70-150 us for that kernel to drain.
-template <int LPP, bool kPaper = false, bool kFma = false, bool kPhys = false>
-__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
+// LPPS: the lane layout that searches the listed blocks (the same 8x8-patch
+// blocks at LPP 2 and 8; LPP 8 needs no spill: 66 VGPRs)
+template <int LPP, bool kPaper = false, bool kFma = false, bool kPhys = false, int LPPS = LPP>
+__global__ void __launch_bounds__(kThreads<LPPS>) __attribute__((amdgpu_waves_per_eu(kWaves<LPPS, LPPS != LPP>)))
 __attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
 {
-    __shared__ BlockLds<LPP> S;
+    static_assert(kBX<LPPS> == kBX<LPP>, "listed blocks must be blocks of the searching layout");
+    __shared__ BlockLds<LPPS> S;
     const int n = *a.fb_count;
     const int nbx = (a.npw + kBX<LPP> - 1) / kBX<LPP>, nby = (a.nph + kBY - 1) / kBY;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int e = a.fb_list[i];
         const int bx = e % nbx, t = e / nbx;
-        search_block<LPP, true, kPaper, kFma, kPhys>(a, bx, t % nby, t / nby, S);
+        search_block<LPPS, true, kPaper, kFma, kPhys>(a, bx, t % nby, t / nby, S);
         __syncthreads();  // LDS reuse by the next listed block
     }
 }
@@ -1499,7 +1509,14 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
                 launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             else
                 DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
-            if (!DIS_EXP_NO_FB) hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            // (DIS_FB_LPP8, exact modes: the listed blocks searched at 8 lanes
+            // per patch, same bits; tolerance mode at 2, whose contracted sums it
+            // shares)
+            if constexpr (DIS_EXP_NO_FB) {
+            } else if constexpr (DIS_FB_LPP8 && !kFma)
+                hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma, false, 8>), fb_grid, dim3(kThreads<8>), 0, s, a);
+            else
+                hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
         }
@@ -1520,7 +1537,10 @@ static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 gr
     if (L == 2) {
         if (split) {
             hipLaunchKernelGGL((k_search8<2, false, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
-            hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            if (DIS_FB_LPP8)
+                hipLaunchKernelGGL((k_search8_fb<2, false, false, true, 8>), fb_grid, dim3(kThreads<8>), 0, s, a);
+            else
+                hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             hipLaunchKernelGGL((k_search8<2, true, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
         }
