@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 6
+#define DIS_ABI_VERSION 7
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -90,8 +90,8 @@ typedef struct dis_workload {
 
 int dis_abi_version(void);
 const char* dis_last_error(void);
-/* "product", or "experiment" for a measurement build with DIS_EXP_* knock-out
- * switches (wrong values by design; csrc/dis_experiments.h) -- ABI v6 */
+/* "product" (ABI v6; since v7 the sources have no compile-time variants,
+ * so every build is the product build) */
 const char* dis_build_kind(void);
 
 /* Fill *out with the preset's knobs for a W x H input (C = auto rule). */
@@ -143,8 +143,10 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
  * dense flow (W_l*H_l*2). Requires dis_set_debug(ctx, 1) before the calc.
  * DIS_STAGE_FALLBACK (count 1, no debug mode needed): the number of patch
  * blocks of level `level` whose start positions were too spread for the LDS
- * tile and were searched by the fallback kernel in the last calc, summed over
- * the call's sub-batches (`pair` only has to lie in the last batch). */
+ * tile and were searched by the fallback kernel in the last dis_calc_* on this
+ * context (graph replays included), summed over the call's sub-batches (`pair`
+ * only has to lie in the last batch). dis_flow_from_pyramids has no context
+ * and keeps its own counters: a context's count is never changed by it. */
 typedef enum dis_stage {
     DIS_STAGE_IMG0 = 0,
     DIS_STAGE_IMG1 = 1,
@@ -166,15 +168,14 @@ dis_status dis_set_concurrency(dis_ctx* ctx, int streams);
  * lanes per patch on the rest), 1 = generic kernels only, 2 / 3 / 4 / 5 = the
  * patch_size-8 search with 4 / 2 / 8 / 1 lanes per patch on every level (5:
  * where the 16x8-patch block fits, grid step <= 7; else 2), 6 = one wave64
- * per patch (lane = pixel) on every exact non-paper level (else 2), 7 = auto
- * with one launch per coarse level (what 0 does in the default build), 8 =
- * auto with the coarse levels at 8 lanes per patch fused into one launch
- * (k_search8_head, ABI v6; measured 0.6-1.0 % slower per step, so not the
- * default), 9 = 2 lanes per patch on every level with the usable LDS tile
+ * per patch (lane = pixel) on every exact non-paper level (else 2), 9 = 2
+ * lanes per patch on every level with the usable LDS tile
  * capped at 24 rows / columns, so that most patch blocks take the fallback
  * list and kernel (a parity-test switch: natural inputs rarely spread a
  * block's start positions beyond the full tile). All are bit-identical; the
- * switch exists for parity tests and A/B timing. */
+ * switch exists for parity tests and A/B timing. 7 and 8 (ABI v6: one launch
+ * per coarse level, the fused coarse head) were removed in v7 -- the head
+ * measured slower -- and are refused. */
 dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
 
 /* Arithmetic of the patch_size-8 search kernels (ABI v4; no reference

@@ -304,11 +304,9 @@ hipError_t launch_flow_color(const float* flow, int n, int W, int H, float maxmo
     if (e != hipSuccess) return e;
     // fields per chunk: ~128 MB of flow, re-read from the Infinity Cache
     const long long fbytes = a.npix * 8;
-#ifndef DIS_COLOR_CHUNK_MB
-#define DIS_COLOR_CHUNK_MB 128  // r04 A/B (32 x 1080p fields): 32 / 64 / 128 MB chunks 0.41 / 0.36-0.38 / 0.32-0.34 ms
-#endif
-    const int chunk =
-        (int)std::max<long long>(1, std::min<long long>(n, ((long long)DIS_COLOR_CHUNK_MB << 20) / std::max(1LL, fbytes)));
+    // (r04 A/B, 32 x 1080p fields: 32 / 64 / 128 MB chunks 0.41 / 0.36-0.38 / 0.32-0.34 ms)
+    constexpr long long kChunkBytes = 128LL << 20;
+    const int chunk = (int)std::max<long long>(1, std::min<long long>(n, kChunkBytes / std::max(1LL, fbytes)));
     const unsigned mb = (unsigned)std::min<long long>(256, (a.npix + 2LL * kThreads * 8 - 1) / (2LL * kThreads * 8));
     auto chunk_args = [&](int f0) {
         ColorArgs c = a;

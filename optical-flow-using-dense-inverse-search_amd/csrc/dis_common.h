@@ -4,8 +4,6 @@
 // uses float): src/optical_flow.cpp:33-63, src/patch_grid.cpp:17-51.
 #pragma once
 
-#include "dis_experiments.h"  // first: refuses knock-out builds without DIS_EXPERIMENTS
-
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>

@@ -90,6 +90,28 @@ __device__ __forceinline__ LU2 hessian_lu2(float h00, float h01, float h11)
     return lu2_factor(h00, h01, h10, h11);
 }
 
+// Bilinear warp weights and tap base of one sample position
+// (src/patch.cpp:207-267): l = floorf(x), k = floorf(y), a = x - l, b = y - k,
+// X = ceilf(x + 1e-5f) (Q8: the epsilon is a no-op from 256 on).
+struct Warp {
+    float w0, w1, w2, w3;
+    int X, Y;
+};
+
+__device__ __forceinline__ Warp warp_coefs(float x, float y)
+{
+    Warp w;
+    const float l = floorf(x), k = floorf(y);
+    const float a = x - l, b = y - k;
+    w.w0 = (1 - a) * (1 - b);
+    w.w1 = a * (1 - b);
+    w.w2 = b * (1 - a);
+    w.w3 = a * b;
+    w.X = (int)ceilf(x + .00001f);
+    w.Y = (int)ceilf(y + .00001f);
+    return w;
+}
+
 // Densified flow at one level pixel (px, py) (src/patch_grid.cpp:121-182) as a
 // gather: every patch whose ps x ps footprint covers the pixel contributes
 // 0.5*u in patch-id order (gx outer, gy inner), f starts at +0, the weight is
@@ -124,29 +146,14 @@ __device__ __forceinline__ float2 dense_at(const float2* __restrict__ u, int npw
 // x = N, an integer < 2^22 (Sobel magnitude^2 * 64). On that domain the raw
 // v_sqrt_f32 of gfx950 is either RN(sqrt N) or one ulp BELOW it (never above:
 // tools/sqrt_dir, all 2,080,801 N: 1,744,787 exact, 336,014 one ulp low), so
-// only the round-up test is needed (DIS_SQRT_SIDE 1, the default: 4 VALU
-// instead of 8; k_pyr12 98.7 -> 85.4 us per 32 1080p pairs). tools/sqrt_check
-// (a -m gpu test) proves the compiled form equal to sqrtf on every such N.
-#ifndef DIS_SQRT_SIDE
-#define DIS_SQRT_SIDE 1  // 0: both tests; 1 / 2: only the round-up / round-down test
-#endif
+// only the round-up test is needed (4 VALU instead of 8; k_pyr12 98.7 -> 85.4
+// us per 32 1080p pairs). tools/sqrt_check (a -m gpu test) proves the compiled
+// form equal to sqrtf on every such N.
 __device__ __forceinline__ float sqrt_cr(float x)
 {
     const float r = __builtin_amdgcn_sqrtf(x);
-    if constexpr (DIS_SQRT_SIDE == 1) {
-        const float rp = __int_as_float(__float_as_int(r) + 1);
-        return __builtin_fmaf(-rp, r, x) > 0.0f ? rp : r;
-    } else if constexpr (DIS_SQRT_SIDE == 2) {
-        const float rm = __int_as_float(__float_as_int(r) - 1);
-        return __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
-    }
-    const float rm = __int_as_float(__float_as_int(r) - 1);
     const float rp = __int_as_float(__float_as_int(r) + 1);
-    const float em = __builtin_fmaf(-rm, r, x);
-    const float ep = __builtin_fmaf(-rp, r, x);
-    float y = em <= 0.0f ? rm : r;
-    y = ep > 0.0f ? rp : y;
-    return y;
+    return __builtin_fmaf(-rp, r, x) > 0.0f ? rp : r;
 }
 
 // Correctly rounded a / b for a divisor b used many times (the search's
@@ -159,15 +166,11 @@ __device__ __forceinline__ float sqrt_cr(float x)
 // image-scale. a = +-0 keeps q0 (the fma steps would turn -0 into +0);
 // b = 0 gives r = inf and NaN instead of +-inf, which the outlier test
 // resets exactly like the reference's inf.
-#ifndef DIS_DIVPRE_BFI
-#define DIS_DIVPRE_BFI 1
-#endif
 __device__ __forceinline__ float div_pre(float a, float b, float r)
 {
     const float q0 = a * r;
     const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
     const float q2 = __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
-#if DIS_DIVPRE_BFI
     // the sign of q0 on the magnitude of q2 (one v_bfi_b32 instead of a
     // compare and a VCC select): for a != 0 and finite b the two signs agree
     // (sign(a / b) = sign(a * RN(1 / b)), signed zeros of an underflow
@@ -175,9 +178,6 @@ __device__ __forceinline__ float div_pre(float a, float b, float r)
     // have lost while q0's is right -- the bits of `a == 0 ? q0 : q2` for
     // every finite b (the divisors here are finite: patch sums, weights)
     return __int_as_float((__float_as_int(q0) & (int)0x80000000) | (__float_as_int(q2) & 0x7fffffff));
-#else
-    return a == 0.0f ? q0 : q2;
-#endif
 }
 
 // a / b, correctly rounded, for 2^-60 <= b <= 2^60 and a = 0 or

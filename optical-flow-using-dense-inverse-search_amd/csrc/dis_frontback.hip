@@ -28,14 +28,10 @@ namespace {
 // grid: (Wp / T0, Hp / T0, 2 * batch), block 256; z = pair*2 + frame.
 // LEVELS (1..6) is a template parameter so every load loop has a compile-time
 // trip count and all of a thread's loads are in flight at once.
-#ifndef DIS_PYR_NF
-#define DIS_PYR_NF 1  // frames per pyramid workgroup (1: z = 2 * pair + frame; 2: both, measured 7 % slower)
-#endif
-#ifndef DIS_PYR_THREADS
-#define DIS_PYR_THREADS (128 * DIS_PYR_NF)
-#endif
-constexpr int kPyrNF = DIS_PYR_NF;
-constexpr int kPyrT = DIS_PYR_THREADS;  // threads per pyramid workgroup
+// frames per pyramid workgroup: 1 (z = 2 * pair + frame); both frames in one
+// 256-thread workgroup measured 7 % slower
+constexpr int kPyrNF = 1;
+constexpr int kPyrT = 128 * kPyrNF;  // threads per pyramid workgroup
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 
@@ -47,17 +43,6 @@ __device__ __forceinline__ short2v byte_pair(unsigned w0, unsigned w1)
     return __builtin_bit_cast(short2v, __builtin_amdgcn_perm(w1, w0, sel));
 }
 
-#ifdef DIS_PYR_PROF  // experiment (tools/pyr_probe.hip): per-workgroup phase clocks of wave 0
-__device__ unsigned long long* g_pyr_prof;
-#define PYR_MARK(k) \
-    do { \
-        pyr_t[k] = __builtin_readcyclecounter(); \
-    } while (0)
-#else
-#define PYR_MARK(k) \
-    do { \
-    } while (0)
-#endif
 
 // LDS of one pyramid workgroup. u8 staging: tile column c of row r at byte
 // r * SR + CO + c, so the body columns 1..T0 start 4-byte aligned (dword
@@ -95,16 +80,7 @@ __device__ __forceinline__ void pyr_load_rows(const PyramidArgs& a, int tx, int 
         const int f = i >= SS * Q, rem = i - f * SS * Q, r = rem / Q, j = rem - r * Q;
         const int ys = clampi(reflect101(ty - 1 + r, a.Hp) - a.pt, 0, a.H - 1);
         const uint8_t* in = ((f | fsel) ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
-#ifdef DIS_EXP_PYR_NOLOAD  // experiment: no HBM reads (synthetic bytes)
-        const unsigned sy = (unsigned)(ys * 2654435761u + j) & 0x3f3f3f3fu;
-        if constexpr (V == 16)
-            R.body[k] = make_uint4(sy, sy ^ 1u, sy ^ 2u, sy ^ 3u);
-        else
-            R.body[k] = sy;
-        (void)in;
-#else
         R.body[k] = *reinterpret_cast<const typename P::VT*>(in + (size_t)ys * a.stride + (tx - a.pl) + V * j);
-#endif
     }
 #pragma unroll
     for (int k = 0; k < P::KH; ++k) {
@@ -258,11 +234,7 @@ __device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>
                     const short2v q = X[r + 1][c] * c20 + (X[r][c] * c1m1 + X[r + 2][c]);
                     int n;
                     __asm__("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(n) : "v"(q));
-#ifdef DIS_EXP_PYR_RAWSQRT  // experiment: uncorrected sqrt (wrong in the last bit)
-                    m[r][c] = __builtin_amdgcn_sqrtf((float)n);
-#else
                     m[r][c] = sqrt_cr((float)n);  // 8 x the magnitude (scaled below, exactly)
-#endif
                 }
         } else {
             int R[E0 + 2][E0], T[E0 + 2][E0];
@@ -308,11 +280,7 @@ __device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>
                 const float l1 = s * 0.03125f;  // (s / 8) * 0.25, exact
                 const int y1 = B1 * by + i, x1 = B1 * bx + j;
                 buf0[y1 * N1 + x1] = l1;
-#ifdef DIS_EXP_PYR_NOSTORE  // experiment: no level-1 HBM writes (kept live)
-                if (l1 < -1.0f) p1[y1 * a.w[1] + x1] = l1;
-#else
                 p1[y1 * a.w[1] + x1] = l1;
-#endif
             }
     }
 
@@ -336,11 +304,7 @@ __device__ __forceinline__ void pyr_compute(const PyramidArgs& a, PyrLds<LEVELS>
             s = s + p[ns + 1];
             const float v = s * 0.25f;
             nxt[kk] = v;
-#ifdef DIS_EXP_PYR_NOSMALLSTORE  // experiment: no level >= 2 HBM writes (kept live)
-            if (v < -1.0f) pl[y * a.w[l] + x] = v;
-#else
             pl[y * a.w[l] + x] = v;
-#endif
         }
     }
 }
@@ -353,7 +317,6 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     const int tid = threadIdx.x;
     if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
         for (int i = tid; i < a.nzero; i += blockDim.x) a.zero[i] = 0;
-        for (int i = tid; i < a.nzero2; i += blockDim.x) a.zero2[i] = 0;
     }
     // XCD-aware tile order: the dispatcher deals linear block ids round-robin
     // to the 8 XCDs; remap so each XCD gets a contiguous run of tiles along x
@@ -361,13 +324,6 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     const int nbx = gridDim.x, nby = gridDim.y;
     const int nb = nbx * nby * gridDim.z;
     const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
-#ifdef DIS_PYR_PROF
-    // clocks kept in registers and stored at the end (a store here would be
-    // waited for by the first vmcnt wait)
-    unsigned long long pyr_t[5];
-    const unsigned long long pyr_w0 = wall_clock64();
-    PYR_MARK(0);
-#endif
     const int per = nb / 8;
     const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
     // (divisions run on the vector unit: make the results provably uniform)
@@ -379,29 +335,8 @@ __global__ void __launch_bounds__(kPyrT) __attribute__((amdgpu_waves_per_eu(8)))
     // (kPyrNF 1) z = 2 * pair + frame
     const int pair = kPyrNF == 2 ? bz : bz >> 1, fsel = kPyrNF == 2 ? 0 : bz & 1;
     pyr_stage(a, S, tx, ty, pair, fsel, tid);
-    PYR_MARK(1);
     __syncthreads();
-    PYR_MARK(2);
-#ifdef DIS_EXP_PYR_LOADONLY  // experiment (pyr_probe): staging only
-    if (S.srcs[0][tid] == 255 && S.srcs[1][tid] == 254) a.img0[tid] = 1.0f;
-    PYR_MARK(3);
-#else
     pyr_compute(a, S, tx, ty, pair, fsel, tid);
-    PYR_MARK(3);
-#endif
-    PYR_MARK(4);
-#ifdef DIS_PYR_PROF
-    if (tid == 0) {
-        unsigned hw, xcc;
-        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* o = g_pyr_prof + (size_t)lin * 8;
-        for (int k = 0; k < 5; ++k) o[k] = pyr_t[k];
-        o[5] = wall_clock64();
-        o[6] = ((unsigned long long)xcc << 32) | hw;
-        o[7] = pyr_w0;
-    }
-#endif
 }
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t)
@@ -425,10 +360,9 @@ hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing
 // ---------------------------------------------------------------------------
 namespace {
 
-#ifndef DIS_OUT_TH
-#define DIS_OUT_TH 64  // measured: 64 rows beat 16 by 2.3% of the step (F >= 1)
-#endif
-constexpr int kOutTW = 64, kOutTH = DIS_OUT_TH;  // full-resolution output tile per workgroup
+// full-resolution output tile per workgroup (measured: 64 rows beat 16 by
+// 2.3 % of the step at F >= 1)
+constexpr int kOutTW = 64, kOutTH = 64;
 
 // LDS shapes per instantiation: level-F window (F == 0 is the widest; F >= 1
 // needs half the tile + the interpolation halo) and the staged patch block for
@@ -467,18 +401,12 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 }
 
 
-// one float4 (two output pixels) of the flow. DIS_OUT_NT: streaming
-// (non-temporal) stores -- the one-stream kernel trace gets faster (the next
-// call's k_pyramid 122 -> 112 us: the flow no longer displaces its frames in
-// L2 / MALL), but the two-sub-batch step measured 2-3 % slower
+// one float4 (two output pixels) of the flow. (Streaming, non-temporal
+// stores made the one-stream kernel trace faster -- the next call's pyramid
+// no longer evicted -- but the two-sub-batch step 2-3 % slower: DESIGN.md 3.)
 __device__ __forceinline__ void store_flow2(float2* dst, float2 o0, float2 o1)
 {
-#ifdef DIS_OUT_NT
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store((f4v){o0.x, o0.y, o1.x, o1.y}, reinterpret_cast<f4v*>(dst));
-#else
     *reinterpret_cast<float4*>(dst) = make_float4(o0.x, o0.y, o1.x, o1.y);
-#endif
 }
 
 // Output rows of an interior tile at F == 1 (every tap unclamped, every column
@@ -533,19 +461,6 @@ __device__ __forceinline__ void out_rows_f1(const OutputArgs& a, const float2* d
 // K = ceil(ps / steps) bounds the covering patches per axis, so the gather is
 // an unrolled, predicated K x K loop (no divergent loops).
 template <bool UPSAMPLE, int K, bool kPaper = false>
-#ifdef DIS_STAMP  // diagnostic: every workgroup's end clock, max per call (see kStampN)
-#define OUT_STAMP()                                                                                   \
-    do {                                                                                              \
-        if (a.stamp && threadIdx.x == 0) {                                                            \
-            const unsigned long long n = __hip_atomic_load(&a.stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
-            atomicMax(&a.stamp[1 + kStampN + ((n - 1) % kStampN)], wall_clock64());                   \
-        }                                                                                             \
-    } while (0)
-#else
-#define OUT_STAMP() \
-    do {            \
-    } while (0)
-#endif
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
     constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
@@ -617,12 +532,6 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const float rrw = __builtin_amdgcn_rcpf((float)rw);  // k / rw by floordiv_r: exact for k < 2^12
     for (int k = tid; k < rw * rh; k += 256) {
         const int r = floordiv_r(k, rrw), c = k - r * rw;
-#ifdef DIS_EXP_OUT_NODENSE  // experiment: no densify arithmetic (wrong values)
-        if (true) {
-            dense[r * kOutSW + c] = pu[k % (kOutPX * kOutPY)];
-            continue;
-        }
-#endif
         // dense value: contributions in patch-id order, f from +0; masked
         // terms add +0, an exact no-op (f is never -0)
         const int2 xr = cr[c], yr = rr[r];
@@ -686,7 +595,6 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 
     constexpr int RPT = kOutTH / 8;  // output rows per thread
     const int px = ox + (tid & 31) * 2, py = oy + (tid >> 5) * RPT;
-#ifndef DIS_EXP_OUT_NOUPS
     if constexpr (UPSAMPLE) {
         const int xh = ox + kOutTW - 1 + a.pad_left, yh = oy + kOutTH - 1 + a.pad_top;
         if (a.F == 1 && a.vec_store && ox + kOutTW <= a.W && oy + kOutTH <= a.H && ox + a.pad_left >= 1 &&
@@ -698,23 +606,14 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                 case 2: out_rows_f1<1, 0, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
                 default: out_rows_f1<1, 1, kOutSW, RPT>(a, dense, i0, j0, px, py, pair); break;
             }
-            OUT_STAMP();
             return;
         }
     }
-#endif
 #pragma unroll
     for (int dy = 0; dy < RPT; ++dy) {
         const int y = py + dy;
         if (y >= a.H) continue;
         float2 o[2];
-#ifdef DIS_EXP_OUT_NOUPS  // experiment: no interpolation arithmetic (wrong values)
-        if (true) {
-            const float2* row = dense + ((y - oy) >> 1) * kOutSW + ((px - ox) >> 1);
-            o[0] = row[0];
-            o[1] = row[1];
-        } else
-#endif
         if (UPSAMPLE) {
             int yi;
             float yf;
@@ -762,7 +661,6 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             dst[0] = o[0];
         }
     }
-    OUT_STAMP();
 }
 
 bool output_fits(const OutputArgs& a)

@@ -45,16 +45,6 @@ struct SearchArgs {
 
 // Fast patch-size-8 search (dis_search8.hip): gradients fused from the level
 // image, init fused from the coarser level's patch displacements.
-#ifndef DIS_FB_MERGED
-#define DIS_FB_MERGED 0  // LPP 2 levels: fallback workers inside the search launch (no k_search8_fb)
-#endif
-#ifndef DIS_FB_SPREAD
-#define DIS_FB_SPREAD 1
-#endif
-// verdict counters of the in-launch fallback workers (Search8Args::fb_decided):
-// one per XCD, on separate 128-byte lines
-constexpr int kFbSlots = DIS_FB_SPREAD ? 8 : 1, kFbSlotStride = DIS_FB_SPREAD ? 32 : 1;
-
 struct Search8Args {
     const float* img0;        // frame-0 level planes (stack)
     const float* img1;        // frame-1 level planes (stack)
@@ -76,10 +66,6 @@ struct Search8Args {
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline
-    int* fb_decided;          // non-null (LPP 2): the list is searched by fb_wgs workgroups appended
-                              //   (kFbSlots counters kFbSlotStride ints apart: workgroup id mod 8)
-    int fb_wgs;               //   to the launch (1-D grid), which start once all blocks counted
-                              //   their verdict here (zeroed before the launch); no k_search8_fb
     int paper;                // template-subtracted residual (k_search8<.., kPaper>)
     const float2* u_init;     // non-null (paper mode): per-patch initial u from k_paper_init, patch-id
     long long init_stride;    //   order, float2 per pair
@@ -144,11 +130,8 @@ struct PyramidArgs {
     int w[kMaxLevels];          // plane width per level
     int* zero;                  // nzero ints set to 0 by workgroup 0 (the searches' fallback counts)
     int nzero;
-    int* zero2;                 // nzero2 more (the fused head's counters, k_search8_head), or none
-    int nzero2;
     int dword_ok;               // I0/I1, stride, pair_stride and pad_left 4-byte aligned: dword row loads
     int qword_ok;               // ... and 16-byte aligned, pad_left a multiple of 16: 16-byte row loads
-    unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call start clocks, else null
     int vec_st;                 // k_pyr12: level-1 / level-2 rows 16-byte aligned (W_2 % 4 == 0; set by launch_pyramid2)
 };
 
@@ -166,12 +149,7 @@ struct OutputArgs {
     const float* img0;  // level-F planes of pair 0 (pre-offset), pair stride plane_stride
     const float* img1;
     long long plane_stride;
-    unsigned long long* stamp;  // diagnostic builds (DIS_STAMP) only: per-call end clocks, else null
 };
-
-// DIS_STAMP layout per sub-batch stream: [0] call counter, [1 .. kStampN]
-// k_pyr12 start clocks, [1 + kStampN .. 2 kStampN] k_output end clocks (s_memrealtime, 100 MHz)
-constexpr int kStampN = 4096;
 
 hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing t = {});
 // the same planes by two streaming kernels (dis_pyramid.hip): levels 1-2 from
@@ -190,24 +168,8 @@ int search8_tile_stride(int steps, int lanes_per_patch);
 int search8_tile_quad(int steps, int lanes_per_patch);  // LPP 2: 4 x 4-patch half-waves (Search8Args.quad)
 bool search8_lpp1_fits(int steps);
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
-
-// The coarse head in one launch (dis_search8.hip k_search8_head): levels
-// C .. C - nlev + 1, every one at 8 lanes per patch, workgroups ordered level
-// by level (coarsest first, pairs in order); a block of level i starts once
-// every block of its pair at level i - 1 has finished (per-(level, pair)
-// counters `done`, zeroed before the launch) -- the coarse-to-fine order of
-// src/optical_flow.cpp:67-91 without a kernel boundary between the levels.
-constexpr int kHeadMax = 6;
-struct HeadArgs {
-    Search8Args lv[kHeadMax];  // per head level, coarsest first (lanes_per_patch 8)
-    int nbx[kHeadMax], nby[kHeadMax];  // blocks per pair
-    int start[kHeadMax + 1];   // first workgroup of each level
-    int nlev, batch;
-    int* done;                 // [level][pair] finished blocks
-};
-hipError_t launch_search8_head(const HeadArgs& h, hipStream_t s, Timing t = {});
-// blocks per pair of an 8-lanes-per-patch level (8 x 8 patches per block)
-inline int search8_blocks8(int npw, int nph) { return ((npw + 7) / 8) * ((nph + 7) / 8); }
+// one wave64 per patch (dis_search_wave.hip; lanes_per_patch 64, variant 6)
+hipError_t launch_search_wave(const Search8Args& a, int batch, hipStream_t s, Timing t = {});
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s);
 hipError_t launch_upsample(const UpsampleArgs& a, int batch, hipStream_t s);
 

@@ -121,72 +121,28 @@ __device__ __forceinline__ void block4(const unsigned (&p)[NR], const unsigned (
     o.l2 = s * 0.25f;
 }
 
-// grid: (ceil(W2 / 256), ceil(H2 / RW), 2 * batch) waves; z = 2 * pair +
-// frame. Lane = 4 consecutive level-2 pixels of rows RW y .. RW y + RW - 1 =
-// level-0 columns x0 .. x0 + 15 (x0 = 16 g), window columns x0 - 1 .. x0 + 16,
-// rows 4 RW y - 1 .. 4 RW y + 4 RW: the 2 halo rows are read once per RW
-// level-2 rows (RW 1: 6 rows per 4, 1.5x the frame bytes; RW 2: 1.25x).
-#ifndef DIS_PYR12_XCD
-#define DIS_PYR12_XCD 0  // r03 A/B: HBM bytes 397 -> 300 MB per 32 pairs, but 98 -> 115 us
-#endif
-#ifndef DIS_PYR12_CHUNK
-#define DIS_PYR12_CHUNK 8  // DIS_PYR12_XCD 2: level-2 rows per XCD chunk
-#endif
-#ifndef DIS_PYR12_ROWS
-#define DIS_PYR12_ROWS 1
-#endif
-#ifndef DIS_PYR12_WAVES
-#define DIS_PYR12_WAVES (DIS_PYR12_ROWS == 1 ? 5 : 4)  // min waves per SIMD (RW 1: 91 VGPRs, no spills)
-#endif
-#ifndef DIS_PYR12_WG
-#define DIS_PYR12_WG 1  // waves per workgroup, stacked vertically (same CU: the shared halo rows hit in L1/L2)
-#endif
-constexpr int kPyrRW = DIS_PYR12_ROWS, kPyrWG = DIS_PYR12_WG;
-__global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_eu(DIS_PYR12_WAVES))) k_pyr12(PyramidArgs a)
+// grid: (ceil(W2 / 256), H2, 2 * batch) waves; z = 2 * pair + frame. Lane =
+// 4 consecutive level-2 pixels of row y = level-0 columns x0 .. x0 + 15
+// (x0 = 16 g), window columns x0 - 1 .. x0 + 16, rows 4 y - 1 .. 4 y + 4: the
+// 2 halo rows are read once per level-2 row (6 rows per 4, 1.5x the frame
+// bytes). Waves in plain order: every order that keeps a wave's vertical
+// neighbours on its XCD (XCD remap, chunked remap, 2 / 4 / 8 stacked waves
+// per workgroup) or carries the halo rows in registers (2 / 4 rows per wave)
+// cut the bytes toward the algorithmic 300 MB per 32 pairs and lost time
+// (DRAM locality, not bytes, sets this kernel's rate).
+constexpr int kPyrRW = 1;  // level-2 rows per wave
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) k_pyr12(PyramidArgs a)
 {
     constexpr int RW = kPyrRW, NR = 4 * RW + 2;
     const int lane = threadIdx.x & 63;
     const int W2 = a.w[2], H2 = a.Hp >> 2;
-#if DIS_PYR12_XCD
-    // XCD-aware wave order (off: measured slower, see the macro): the
-    // dispatcher deals linear workgroup ids round-robin to the 8 XCDs; remap
-    // so each XCD walks a contiguous run of rows and the two level-0 halo rows
-    // a wave shares with the next row's wave are read from HBM once
-    const int nbx = gridDim.x, nby = gridDim.y, nb = nbx * nby * gridDim.z;
-    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
-#if DIS_PYR12_XCD == 2
-    // chunked: XCD k takes chunks of CH consecutive waves (DIS_PYR12_CHUNK
-    // rows x the row's waves), the 8 XCDs neighbouring chunks, so the waves in
-    // flight still cover one compact band of the frames (DRAM locality of the
-    // plain order) while vertically adjacent waves mostly share an L2
-    const int CH = DIS_PYR12_CHUNK * nbx, grp = 8 * CH;
-    const int j = lin >> 3, k = lin & 7;
-    const int t = lin < nb / grp * grp ? (j / CH) * grp + k * CH + j % CH : lin;
-#else
-    const int per = nb / 8;
-    const int t = lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
-#endif
-    const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
-    const int yb = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
-    const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
-#else
-    const int bx = blockIdx.x, bz = blockIdx.z;
-    const int yb = kPyrWG == 1 ? blockIdx.y : blockIdx.y * kPyrWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (kPyrWG > 1 && RW * yb >= H2) return;
-#endif
+    const int bx = blockIdx.x, bz = blockIdx.z, yb = blockIdx.y;
     const int y2b = RW * yb;  // first level-2 row of the wave
     const int g = bx * 64 + lane;  // lane's group of 4 level-2 pixels
     const int pair = bz >> 1, frame = bz & 1;
     if (bx == 0 && yb == 0 && bz == 0) {
         for (int i = lane; i < a.nzero; i += 64) a.zero[i] = 0;
-        for (int i = lane; i < a.nzero2; i += 64) a.zero2[i] = 0;
     }
-#ifdef DIS_STAMP
-    if (a.stamp && bx == 0 && yb == 0 && bz == 0 && lane == 0) {
-        const unsigned long long n = atomicAdd(&a.stamp[0], 1ull);
-        a.stamp[1 + (n % kStampN)] = wall_clock64();
-    }
-#endif
     const uint8_t* in = (frame ? a.I1 : a.I0) + (size_t)pair * a.pair_stride;
     const int ng = (W2 + 3) >> 2;                 // groups per row
     const int gc = g < ng ? g : ng - 1;           // idle lanes mirror the last group (loads stay in bounds)
@@ -306,64 +262,6 @@ __global__ void __launch_bounds__(64 * kPyrWG) __attribute__((amdgpu_waves_per_e
     if constexpr (RW > 3) level_row(std::integral_constant<int, 3>{});
 }
 
-// grid: (W2 / T2, H2 / T2, 2 * batch), T2 = 2^(L-2) level-2 pixels per tile
-// edge; one wave per tile computes levels 3..L in LDS
-#ifndef DIS_TAIL_TPW
-#define DIS_TAIL_TPW 2  // level-2 tiles per wave, loads in flight together (r03: 1 / 2 / 3 / 5 -> 20.2 / 14.0 / 16.1 / 16.8 us)
-#endif
-template <int L, int TPW>
-__global__ void __launch_bounds__(64) k_pyr_tail(PyramidArgs a)
-{
-    constexpr int T2 = 1 << (L - 2), N2 = T2 * T2;
-    constexpr int PER = (N2 + 63) / 64;
-    constexpr int NB = N2 / 4 > 0 ? N2 / 4 : 1;
-    __shared__ float buf[TPW][2][NB];  // level l of tile t at buf[t][l & 1]
-    __shared__ float src[TPW][N2];     // the level-2 tiles
-    const int lane = threadIdx.x;
-    const int pair = blockIdx.z >> 1, frame = blockIdx.z & 1;
-    float* planes = (frame ? a.img1 : a.img0) + (size_t)pair * a.plane_stride;
-    const int ntx = a.w[2] / T2;                              // tiles per tile row
-    const int t0 = blockIdx.x * TPW, ty = blockIdx.y * T2;   // first tile, level-2 row origin
-    const float* p2 = planes + a.off[2] + (size_t)ty * a.w[2];
-    float v[TPW][PER];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = lane + 64 * k;
-            v[t][k] = (t0 + t < ntx && i < N2) ? p2[(size_t)(i / T2) * a.w[2] + (t0 + t) * T2 + (i % T2)] : 0.0f;
-        }
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = lane + 64 * k;
-            if (i < N2) src[t][i] = v[t][k];
-        }
-    __syncthreads();
-#pragma unroll
-    for (int l = 3; l <= L; ++l) {
-        const int ns = T2 >> (l - 3), nd = ns / 2;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            if (t0 + t >= ntx) break;  // uniform
-            const float* cur = l == 3 ? src[t] : buf[t][(l - 1) & 1];
-            float* nxt = buf[t][l & 1];
-            const int tx = (t0 + t) * T2;
-            for (int k = lane; k < nd * nd; k += 64) {
-                const int y = k / nd, x = k - y * nd;
-                const float* p = cur + (2 * y) * ns + 2 * x;
-                float s = p[0] + p[1];
-                s = s + p[ns];
-                s = s + p[ns + 1];
-                const float val = s * 0.25f;
-                nxt[k] = val;
-                planes[a.off[l] + (size_t)((ty >> (l - 2)) + y) * a.w[l] + (tx >> (l - 2)) + x] = val;
-            }
-        }
-        __syncthreads();
-    }
-}
 
 // k_pyr_tail_reg<L, TPW>: the same levels 3..L without LDS or barriers. One
 // wave per TPW horizontally adjacent 16 x 16 level-2 super-tiles; lane
@@ -454,7 +352,7 @@ bool pyramid2_fits(const PyramidArgs& a)
 
 hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timing t)
 {
-    if (!pyramid2_fits(a) || (a.nzero2 > 0 && !a.zero2)) return hipErrorInvalidValue;
+    if (!pyramid2_fits(a)) return hipErrorInvalidValue;
     const int W2 = a.Wp >> 2, H2 = a.Hp >> 2;
     if (a.w[2] != W2) return hipErrorInvalidValue;
     const int nrw = (H2 + kPyrRW - 1) / kPyrRW;  // waves per column
@@ -463,30 +361,15 @@ hipError_t launch_pyramid2(const PyramidArgs& a, int batch, hipStream_t s, Timin
     // offsets are multiples of 4: Wp, Hp % 4 == 0): 16-byte stores need W_2 % 4 == 0
     // (with C = 2 or 3, Wp is only a multiple of 4 or 8)
     b.vec_st = W2 % 4 == 0;
-    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, (nrw + kPyrWG - 1) / kPyrWG, 2 * batch), dim3(64 * kPyrWG), 0, s, b);
-#ifndef DIS_TAIL_REG
-#define DIS_TAIL_REG 1
-#endif
-#ifndef DIS_TAIL_REG_TPW
-#define DIS_TAIL_REG_TPW 2
-#endif
-    if (a.levels >= 3 && DIS_TAIL_REG) {
-        constexpr int TPW = DIS_TAIL_REG_TPW;
+    DIS_LAUNCH(t, k_pyr12, dim3((W2 + 255) / 256, nrw, 2 * batch), dim3(64), 0, s, b);
+    if (a.levels >= 3) {
+        constexpr int TPW = 2;  // 16 x 16 level-2 super-tiles per wave, loads in flight together
         const dim3 grid(((W2 + 15) / 16 + TPW - 1) / TPW, (H2 + 15) / 16, 2 * batch);
         switch (a.levels) {
             case 3: hipLaunchKernelGGL((k_pyr_tail_reg<3, TPW>), grid, dim3(64), 0, s, a); break;
             case 4: hipLaunchKernelGGL((k_pyr_tail_reg<4, TPW>), grid, dim3(64), 0, s, a); break;
             case 5: hipLaunchKernelGGL((k_pyr_tail_reg<5, TPW>), grid, dim3(64), 0, s, a); break;
             default: hipLaunchKernelGGL((k_pyr_tail_reg<6, TPW>), grid, dim3(64), 0, s, a); break;
-        }
-    } else if (a.levels >= 3) {
-        const int T2 = 1 << (a.levels - 2), TPW = DIS_TAIL_TPW;
-        const dim3 grid((W2 / T2 + TPW - 1) / TPW, H2 / T2, 2 * batch);
-        switch (a.levels) {
-            case 3: hipLaunchKernelGGL((k_pyr_tail<3, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
-            case 4: hipLaunchKernelGGL((k_pyr_tail<4, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
-            case 5: hipLaunchKernelGGL((k_pyr_tail<5, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
-            default: hipLaunchKernelGGL((k_pyr_tail<6, DIS_TAIL_TPW>), grid, dim3(64), 0, s, a); break;
         }
     }
     return hipGetLastError();

@@ -99,15 +99,9 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
-#ifndef DIS_LPP8_MAX_PATCHES
-#define DIS_LPP8_MAX_PATCHES 16384  // level patches x pairs up to which 8 lanes/patch is used (A/B: 65536 -2.6%)
-#endif
-#ifndef DIS_LPP_BIG
-#define DIS_LPP_BIG 2               // lanes per patch above both thresholds (1 or 2)
-#endif
-#ifndef DIS_LPP4_MAX_PATCHES
-#define DIS_LPP4_MAX_PATCHES 0      // ... and 4 lanes/patch (above: 2 lanes/patch)
-#endif
+// level patches x pairs up to which 8 lanes per patch is used (A/B: 65536
+// -2.6 %); above it 2 lanes per patch (LPP 1 / 4 measured slower)
+constexpr long long kLpp8MaxPatches = 16384;
 
 // Lanes per patch for the patch_size-8 search at one level. Few patches leave
 // the chip idle and the level is bound by one wave's serial iteration chain:
@@ -115,33 +109,16 @@ bool make_geometry(const dis_params& p, int W, int H, Geometry* g)
 // 2 lanes per patch does the least total work.
 static int search8_lanes(int variant, long long patches, int steps)
 {
-    const int big = (DIS_LPP_BIG == 1 && !dis::search8_lpp1_fits(steps)) ? 2 : DIS_LPP_BIG;
     if (variant == 2) return 4;
     if (variant == 3 || variant == 9) return 2;
     if (variant == 4) return 8;
     if (variant == 5) return dis::search8_lpp1_fits(steps) ? 1 : 2;
     if (variant == 6) return 64;  // one wave per patch (exact, non-paper levels)
-    if (patches <= DIS_LPP8_MAX_PATCHES) return 8;
-    if (patches <= DIS_LPP4_MAX_PATCHES) return 4;
-    return big;
+    return patches <= kLpp8MaxPatches ? 8 : 2;
 }
 
-// per sub-batch: the levels' fallback list counts, then their verdict counters
-constexpr size_t kFbCounters = dis::kMaxLevels * (1 + dis::kFbSlots * dis::kFbSlotStride);
-// the counters a call zeroes (levels 0..C; the verdict counters only when merged)
-constexpr int kFbZero(int C)
-{
-    return DIS_FB_MERGED ? dis::kMaxLevels + (C + 1) * dis::kFbSlots * dis::kFbSlotStride : C + 1;
-}
-#ifndef DIS_PYR2
-#define DIS_PYR2 1  // the two-kernel streaming pyramid (dis_pyramid.hip) where it fits
-#endif
-#ifndef DIS_QUAD_LAYOUT
-#define DIS_QUAD_LAYOUT 1  // LPP-2 4 x 4-patch half-waves where they spread the LDS banks better
-#endif
-#ifndef DIS_SAME_STREAM_SKIP
-#define DIS_SAME_STREAM_SKIP 1
-#endif
+// per sub-batch: the levels' fallback list counts (k_search8_fb)
+constexpr size_t kFbCounters = dis::kMaxLevels;
 
 struct dis_ctx {
     dis_params p;
@@ -156,7 +133,6 @@ struct dis_ctx {
     static constexpr int kMaxSub = 8;
     int nsub = 2;                        // sub-batch streams per calc (dis_set_concurrency)
     int precision = 0;                   // dis_set_precision: DIS_PRECISION_EXACT / _FMA
-    unsigned long long* stamp = nullptr;  // DIS_STAMP diagnostic builds: per-sub-batch call clocks
     hipStream_t sub[kMaxSub] = {};
     hipEvent_t fork = nullptr;
     // end of the previous call's work on its stream: every call first orders
@@ -168,9 +144,8 @@ struct dis_ctx {
     // the next call must wait for `done` unless it is on that same stream
     // (stream order already serialises it; skipping the wait packet saves the
     // inter-call gap)
-    bool needs_wait(hipStream_t s) const { return done_pending && !(DIS_SAME_STREAM_SKIP && s == done_stream); }
+    bool needs_wait(hipStream_t s) const { return done_pending && s != done_stream; }
     hipEvent_t join[kMaxSub] = {};
-    hipEvent_t staged[kMaxSub] = {};  // sub-batch k's pyramid done (pipelined start of k+1)
     // variational refinement: its ~16 launches per fixed-point iteration per level
     // are replayed as one HIP graph per (sub-batch, level), captured on first use
     // (all pointers are context workspace; re-captured when the slice changes)
@@ -195,6 +170,7 @@ struct dis_ctx {
         bool launched = false;
         unsigned long long used = 0;  // LRU clock
         int n = -1, nsub = -1, precision = -1, variant = -1;
+        int subs = 1;  // sub-batches the captured call ran (last_nsub on replay)
         const void *i0 = nullptr, *i1 = nullptr;
         void* flow = nullptr;
         size_t stride = 0, pair_stride = 0;
@@ -210,14 +186,11 @@ struct dis_ctx {
     float* vr_ws = nullptr;  // variational refinement workspace (kVarRefPlanes planes per pair)
     long long vr_plane = 0;
     // patch-search fallback lists (dis_search8.hip k_search8_fb): per sub-batch
-    // k, kFbCounters counters at fb + k * kFbCounters (the levels' list counts,
-    // then the merged build's verdict counters), then per (k, level) a list of
-    // up to blocks(level) * pairs entries at fb + fb_list_off[k][level]
+    // k, kFbCounters list counts (one per level) at fb + k * kFbCounters, then
+    // per (k, level) a list of up to blocks(level) * pairs entries at
+    // fb + fb_list_off[k][level]
     int* fb = nullptr;
     size_t fb_list_off[8][dis::kMaxLevels] = {};
-    // fused coarse head (k_search8_head): per sub-batch kHeadMax x max_batch
-    // finished-block counters, zeroed by the pyramid kernel of each call
-    int* head_done = nullptr;
     uint8_t* in0 = nullptr;  // host-mode input staging
     uint8_t* in1 = nullptr;
     float2* out = nullptr;   // host-mode output staging
@@ -264,7 +237,6 @@ dis_status check_params(const dis_params* p, int W, int H)
 
 void free_ws(dis_ctx* c)
 {
-    hipFree(c->stamp);
     hipFree(c->img0);
     hipFree(c->img1);
     hipFree(c->dx);
@@ -273,8 +245,6 @@ void free_ws(dis_ctx* c)
     hipFree(c->dense);
     hipFree(c->fb);
     c->fb = nullptr;
-    hipFree(c->head_done);
-    c->head_done = nullptr;
     hipFree(c->vr_ws);
     c->vr_ws = nullptr;
     hipFree(c->in0);
@@ -333,10 +303,6 @@ int upsample_xmax(const dis::Geometry& g)
     }
     return g.Wp;
 }
-
-#ifndef DIS_VR_GRAPH
-#define DIS_VR_GRAPH 1  // replay each level's refinement launches as a HIP graph
-#endif
 
 constexpr int kStageFront = 1000, kStageBack = -1000;  // other stages: the level index
 
@@ -427,43 +393,15 @@ dis::DensifyArgs densify_args(const dis_ctx* c, int l, const float* img0, const 
     return d;
 }
 
-#ifndef DIS_HEAD
-// the coarse head (levels at 8 lanes per patch) as one launch (k_search8_head)
-// by default; r04 step A/Bs against one launch per level (variant 7):
-// 1.431 / 1.423 and 1.416 / 1.402 ms -- the head's waiting blocks hold CU
-// slots the other sub-batch's search could use -- so off; variant 8 selects it
-#define DIS_HEAD 0
-#endif
-
-// Lowest level of the fused coarse head for a sub-batch of n pairs, or C + 1
-// when there is none: the run of levels C, C-1, ... that search at 8 lanes per
-// patch (at most kHeadMax, at least two), on the plain fast path (patch size
-// 8, no paper mode, refinement or debug dumps). Variant 8 selects it, variant
-// 7 never uses it, the auto variant 0 when built with DIS_HEAD=1.
-int head_lo(const dis_ctx* c, int n)
-{
-    const dis::Geometry& g = c->g;
-    const int none = g.C + 1;
-    const bool want = c->variant == 8 || (DIS_HEAD && c->variant != 1 && c->variant != 6 && c->variant != 7);
-    if (!want || g.ps != 8 || c->debug || c->p.paper_mode || c->p.var_refine_iters > 0 || !c->head_done)
-        return none;
-    int l = g.C;
-    while (l >= g.F && g.C - l + 1 <= dis::kHeadMax &&
-           search8_lanes(c->variant, (long long)g.lv[l].npw * g.lv[l].nph * n, g.lv[l].steps) == 8)
-        --l;
-    return g.C - l >= 2 ? l + 1 : none;
-}
-
 // One stage of the path for n pairs already resident in device memory: the
 // front end (pyramid), one level (search, and densify + refinement when on),
 // or the back end (output). run_batches issues the stages stage-major across
 // the sub-batches, so every sub-batch's next kernels are queued early even
 // when the host is slow to enqueue a long stage.
 dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, const uint8_t* I1, size_t stride,
-                     size_t pair_stride, float2* flow, hipStream_t s, int stage, hipEvent_t wait_pyr = nullptr,
-                     hipEvent_t pyr_done = nullptr, bool capturing = false)
+                     size_t pair_stride, float2* flow, hipStream_t s, int stage)
 {
-    // this sub-batch's fallback counts, then its verdict counts (k_search8's fallback workers)
+    // this sub-batch's fallback counts (one per level)
     int* const fb_count = c->fb + (size_t)sub * kFbCounters;
     const dis::Geometry& g = c->g;
     // this sub-batch's slice of the workspace (pairs p0 .. p0+n-1)
@@ -476,7 +414,6 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     const bool fast = g.ps == 8 && c->variant != 1;
     const bool vr = c->p.var_refine_iters > 0;
     const bool paper = c->p.paper_mode != 0;
-    if (stage == kStageFront && wait_pyr) DIS_HIP(hipStreamWaitEvent(s, wait_pyr, 0));
     if (stage == kStageFront) {
         if (fast && g.C >= 1) {
             dis::PyramidArgs pa{};
@@ -496,12 +433,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             pa.levels = std::min(g.C, 6);
             pa.write_l0 = (g.F == 0 || c->debug) ? 1 : 0;
             pa.zero = fb_count;
-            pa.nzero = kFbZero(g.C);
-            if (head_lo(c, n) <= g.C) {  // the fused head's counters of this sub-batch
-                pa.zero2 = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
-                pa.nzero2 = (g.C + 1 - head_lo(c, n)) * n;
-            }
-            pa.stamp = c->stamp ? c->stamp + (size_t)sub * (1 + 2 * dis::kStampN) : nullptr;
+            pa.nzero = g.C + 1;
             pa.dword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
                             (n > 1 ? pair_stride : 0) | (size_t)g.pad_left) & 3) == 0;
             pa.qword_ok = ((reinterpret_cast<uintptr_t>(I0) | reinterpret_cast<uintptr_t>(I1) | stride |
@@ -510,15 +442,14 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
                 pa.off[l] = g.lv[l].plane_off;
                 pa.w[l] = g.lv[l].W;
             }
-            if (DIS_PYR2 && dis::pyramid2_fits(pa))
+            if (dis::pyramid2_fits(pa))  // the two-kernel streaming pyramid (dis_pyramid.hip)
                 DIS_HIP(dis::launch_pyramid2(pa, n, s, timing(c, 0)));
             else
                 DIS_HIP(dis::launch_pyramid(pa, n, s, timing(c, 0)));
             for (int l = pa.levels + 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
-            if (pyr_done) DIS_HIP(hipEventRecord(pyr_done, s));
         } else {
             // (zeroed on every path: DIS_STAGE_FALLBACK reports them after any calc)
-            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * kFbZero(g.C), s));
+            DIS_HIP(hipMemsetAsync(fb_count, 0, sizeof(int) * (g.C + 1), s));
             DIS_HIP(dis::launch_level0(I0, I1, stride, pair_stride, g, img0, img1, n, s));
             for (int l = 1; l <= g.C; ++l) DIS_HIP(dis::launch_down2(g, l, img0, img1, n, s));
         }
@@ -555,37 +486,19 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         b.thr_sq = sqrt_threshold((float)g.ps / 2);
         b.lanes_per_patch = search8_lanes(c->variant, (long long)Lq.npw * Lq.nph * n, Lq.steps);
         b.tile_stride = dis::search8_tile_stride(Lq.steps, b.lanes_per_patch);
-        b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(Lq.steps, b.lanes_per_patch) : 0;
+        b.quad = dis::search8_tile_quad(Lq.steps, b.lanes_per_patch);
         b.tile_cap = c->variant == 9 ? 24 : 0;  // variant 9: most blocks through the fallback list
         b.fb_count = fb_count + lq;
         b.fb_list = c->fb + c->fb_list_off[sub][lq];
-        if (DIS_FB_MERGED && b.lanes_per_patch == 2) b.fb_decided = fb_count + dis::kMaxLevels + lq * dis::kFbSlots * dis::kFbSlotStride;
         b.paper = paper ? 1 : 0;
         b.iters = g.iters;
         b.norm = g.norm;
         b.fma = (c->precision == DIS_PRECISION_FMA && !paper) ? 1 : 0;
         return b;
     };
-    const int hl = fast ? head_lo(c, n) : g.C + 1;
     for (int l = g.C; l >= g.F; --l) {  // src/optical_flow.cpp:67-91
         if (l != stage) continue;
         const dis::LevelGeom& L = g.lv[l];
-        if (l >= hl) {  // the fused coarse head: all of it at stage C, nothing at its other levels
-            if (l < g.C) continue;
-            dis::HeadArgs h{};
-            h.nlev = g.C - hl + 1;
-            h.batch = n;
-            h.done = c->head_done + (size_t)sub * dis::kHeadMax * c->max_batch;
-            for (int i = 0; i < h.nlev; ++i) {
-                const dis::LevelGeom& Li = g.lv[g.C - i];
-                h.lv[i] = make_s8(g.C - i);
-                h.nbx[i] = (Li.npw + 7) / 8;
-                h.nby[i] = (Li.nph + 7) / 8;
-                h.start[i + 1] = h.start[i] + h.nbx[i] * h.nby[i] * n;
-            }
-            DIS_HIP(dis::launch_search8_head(h, s, timing(c, 1, hl == g.F ? 2 : -1)));
-            continue;
-        }
         dis::SearchArgs a{};
         a.img0 = img0;
         a.img1 = img1;
@@ -649,15 +562,8 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             if (b.lanes_per_patch == 64 && (paper || b.fma)) {  // exact, non-paper only
                 b.lanes_per_patch = 2;
                 b.tile_stride = dis::search8_tile_stride(L.steps, 2);
-                b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, 2) : 0;
+                b.quad = dis::search8_tile_quad(L.steps, 2);
             }
-#ifdef DIS_EXP_SKIP_HEAD  // experiment (wrong values): levels >= DIS_EXP_SKIP_HEAD not searched, u = 0
-            if (l >= DIS_EXP_SKIP_HEAD && l > g.F) {
-                DIS_HIP(hipMemset2DAsync(b.u_out, (size_t)g.u_stride * sizeof(float2), 0,
-                                         (size_t)L.n * sizeof(float2), n, s));
-                continue;
-            }
-#endif
             DIS_HIP(dis::launch_search8(b, n, s, timing(c, 1, l == g.F ? 2 : -1)));
         } else {
             DIS_HIP(dis::launch_search_generic(a, g.ps, n, s, timing(c, 1, l == g.F ? 2 : -1)));
@@ -681,11 +587,7 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             v.W = L.W;
             v.H = L.H;
             v.iters = c->p.var_refine_iters;
-            auto& G = c->vrg[sub][l];
-            if (!DIS_VR_GRAPH) {
-                DIS_HIP(dis::launch_var_refine(v, n, s));
-                continue;
-            }
+            auto& G = c->vrg[sub][l];  // the level's launches replayed as one HIP graph
             if (G.n != n || G.p0 != p0) {
                 if (G.exec) hipGraphExecDestroy(G.exec);
                 G.exec = nullptr;
@@ -733,7 +635,6 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         o.img0 = img0 + LF.plane_off;
         o.img1 = img1 + LF.plane_off;
         o.plane_stride = g.plane_stride;
-        o.stamp = c->stamp ? c->stamp + (size_t)sub * (1 + 2 * dis::kStampN) : nullptr;
         fused_out = dis::output_fits(o) && !vr;  // refined: the finest dense field exists
     }
     if (fused_out) {
@@ -761,26 +662,12 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
     return DIS_OK;
 }
 
-#ifndef DIS_STAGGER
-#define DIS_STAGGER 0  // measured: lockstep sub-batches 1-3% faster on 1080p MEDIUM (search dominates)
-#endif
-#ifndef DIS_SUB0_CALLER
-#define DIS_SUB0_CALLER 0  // 1: sub-batch 0 on the caller's stream (see run_batches)
-#endif
-#ifndef DIS_STAGE_MAJOR
-#define DIS_STAGE_MAJOR 1
-#endif
-#ifndef DIS_STAGGER_PRIO
-#define DIS_STAGGER_PRIO DIS_STAGGER
-#endif
-
 // Split n pairs into sub-batches on the context's streams (fork from `s`,
 // join back into `s`): pairs are independent, so the latency-bound phases of
 // one sub-batch (coarse levels, kernel tails) overlap the others' work. The
-// sub-batches are pipelined: sub-batch k's (HBM-bound) pyramid starts when
-// k-1's pyramid is done, so it runs beside k-1's coarse levels and search
-// (VALU-bound) instead of contending with the other pyramids for HBM, and
-// k-1's output kernel runs beside k's search.
+// sub-batches run in lockstep (staggered starts, stream priorities and
+// uneven splits measured 1-4.5 % slower: DESIGN.md 7), stages issued
+// stage-major so every sub-batch's next kernels are queued early.
 dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride,
                        size_t pair_stride, float2* flow, hipStream_t s, bool capturing = false)
 {
@@ -796,7 +683,7 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     if (S <= 1) {
         for (int st : stages) {
             StageRange range(st, 0);
-            dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st, nullptr, nullptr, capturing);
+            dis_status r = run_batch(c, 0, n, 0, I0, I1, stride, pair_stride, flow, s, st);
             if (r != DIS_OK) return r;
         }
         c->last_batch = n;
@@ -813,28 +700,18 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     // with sub[1] -- serialising the two sub-batches -- depended on how many
     // streams the process had created before: 15k vs 20k pairs/s at 1080p.
     // The context's own streams are created back to back, on distinct queues.)
-    const int k0 = DIS_SUB0_CALLER ? 1 : 0;
     DIS_HIP(hipEventRecord(c->fork, s));
-    for (int k = k0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+    for (int k = 0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
     const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
-    const bool stage_major = DIS_STAGE_MAJOR;
-    for (size_t i = 0; i < stages.size() * S; ++i) {
-        const int k = stage_major ? (int)(i % S) : (int)(i / stages.size());
-        const int st = stage_major ? stages[i / S] : stages[i % stages.size()];
-#ifdef DIS_EXP_SPLIT0  // experiment: sub-batch 0 takes n / 2 + DIS_EXP_SPLIT0 pairs (two sub-batches)
-        const int a = k == 0 ? 0 : n / 2 + DIS_EXP_SPLIT0, b = k == 0 ? n / 2 + DIS_EXP_SPLIT0 : n;
-#else
+    for (size_t i = 0; i < stages.size() * S; ++i) {  // stage-major
+        const int k = (int)(i % S), st = stages[i / S];
         const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
-#endif
-        hipStream_t sk = k < k0 ? s : c->sub[k];
         StageRange range(st, k);
         dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
-                                 stride, pair_stride, flow + (size_t)a * fpp, sk, st,
-                                 (DIS_STAGGER && k > 0) ? c->staged[k - 1] : nullptr,
-                                 DIS_STAGGER ? c->staged[k] : nullptr, capturing);
+                                 stride, pair_stride, flow + (size_t)a * fpp, c->sub[k], st);
         if (r != DIS_OK) return r;
     }
-    for (int k = k0; k < S; ++k) {
+    for (int k = 0; k < S; ++k) {
         DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
         DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
     }
@@ -939,8 +816,10 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
         G->nsub = c->nsub;
         G->precision = c->precision;
         G->variant = c->variant;
+        G->subs = c->last_nsub;
     }
     G->used = ++c->graph_clock;
+    c->last_nsub = G->subs;  // a replay runs the sub-batches it was captured with (DIS_STAGE_FALLBACK)
     if (c->needs_wait(s)) DIS_HIP(hipStreamWaitEvent(s, c->done, 0));  // the workspace is free
     {
         StageRange range("dis: graph launch");
@@ -970,15 +849,9 @@ bool sub_streams(int device, hipStream_t (&out)[dis_ctx::kMaxSub])
     std::lock_guard<std::mutex> lock(mu);
     auto& v = pools[device];
     if (v.empty()) {
-        // pipelined sub-batches (DIS_STAGGER_PRIO): later sub-batches get the
-        // higher priority, so the workgroups of their latency-bound coarse
-        // levels are dispatched as soon as the earlier sub-batch's retire
-        int prio_lo = 0, prio_hi = 0;
-        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
         for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
             hipStream_t st = nullptr;
-            if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking,
-                                            (DIS_STAGGER_PRIO && k > 0) ? prio_hi : prio_lo) != hipSuccess) {
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
                 for (hipStream_t x : v) hipStreamDestroy(x);
                 v.clear();
                 return false;
@@ -1071,7 +944,7 @@ dis::DensifyArgs densify_level(const dis::Geometry& g, int l, float2* pu, float2
 extern "C" {
 
 int dis_abi_version(void) { return DIS_ABI_VERSION; }
-const char* dis_build_kind(void) { return DIS_BUILD_KIND; }
+const char* dis_build_kind(void) { return "product"; }
 
 const char* dis_last_error(void) { return g_err.c_str(); }
 
@@ -1205,23 +1078,15 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
                 off += (size_t)((g.lv[l].npw + 7) / 8) * ((g.lv[l].nph + 7) / 8) * B;  // 8x8 blocks (the most)
             }
         ok = hipMalloc(&c->fb, sizeof(int) * off) == hipSuccess &&
-             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * kFbCounters) == hipSuccess &&
-             hipMalloc(&c->head_done, sizeof(int) * dis_ctx::kMaxSub * dis::kHeadMax * B) == hipSuccess;
+             hipMemset(c->fb, 0, sizeof(int) * dis_ctx::kMaxSub * kFbCounters) == hipSuccess;
     }
-#ifdef DIS_STAMP  // diagnostic builds: per-call clocks of each sub-batch stream (tools/stamp_probe.py)
-    if (ok && getenv("DIS_STAMP")) {
-        const size_t ns = sizeof(unsigned long long) * dis_ctx::kMaxSub * (1 + 2 * dis::kStampN);
-        ok = hipMalloc(&c->stamp, ns) == hipSuccess && hipMemset(c->stamp, 0, ns) == hipSuccess;
-    }
-#endif
     if (ok && params->var_refine_iters > 0) {
         c->vr_plane = (long long)g.lv[g.F].W * g.lv[g.F].H;  // the largest refined level
         ok = hipMalloc(&c->vr_ws, sizeof(float) * dis::kVarRefPlanes * c->vr_plane * B) == hipSuccess;
     }
     ok = ok && sub_streams(device, c->sub);
     for (int k = 0; ok && k < dis_ctx::kMaxSub; ++k)
-        ok = hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->staged[k], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
     // The capture-only stream exists only under refinement and is created last:
     // HIP assigns streams to its (GPU_MAX_HW_QUEUES = 4) hardware queues round
     // robin at creation, and an extra stream created before sub[] shifted
@@ -1230,10 +1095,8 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
     if (ok) ok = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         free_ws(c);
-        for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+        for (int k = 0; k < dis_ctx::kMaxSub; ++k)
             if (c->join[k]) hipEventDestroy(c->join[k]);
-            if (c->staged[k]) hipEventDestroy(c->staged[k]);
-        }
         if (c->fork) hipEventDestroy(c->fork);
         if (c->done) hipEventDestroy(c->done);
         if (c->cap) hipStreamDestroy(c->cap);
@@ -1255,10 +1118,8 @@ dis_status dis_destroy(dis_ctx* c)
         if (c->join[k]) hipEventSynchronize(c->join[k]);  // context's last join, not the stream
     free_ws(c);
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
-    for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+    for (int k = 0; k < dis_ctx::kMaxSub; ++k)
         if (c->join[k]) hipEventDestroy(c->join[k]);
-        if (c->staged[k]) hipEventDestroy(c->staged[k]);
-    }
     if (c->fork) hipEventDestroy(c->fork);
     if (c->done) hipEventDestroy(c->done);
     for (auto& row : c->vrg)
@@ -1347,7 +1208,8 @@ dis_status dis_set_precision(dis_ctx* c, int mode)
 dis_status dis_set_kernel_variant(dis_ctx* c, int variant)
 {
     if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
-    if (variant < 0 || variant > 9) return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..9");
+    if (variant < 0 || variant > 9 || variant == 7 || variant == 8)
+        return fail(DIS_ERR_INVALID_ARGUMENT, "variant must be 0..6 or 9 (7 and 8 were removed in ABI v7)");
     c->variant = variant;
     return DIS_OK;
 }
@@ -1544,7 +1406,7 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
             b.thr_sq = sqrt_threshold((float)g.ps / 2);
             b.lanes_per_patch = search8_lanes(0, (long long)L.npw * L.nph, L.steps) == 8 ? 8 : 2;
             b.tile_stride = dis::search8_tile_stride(L.steps, b.lanes_per_patch);
-            b.quad = DIS_QUAD_LAYOUT ? dis::search8_tile_quad(L.steps, b.lanes_per_patch) : 0;
+            b.quad = dis::search8_tile_quad(L.steps, b.lanes_per_patch);
             b.fb_count = w.fb + l;
             b.fb_list = w.fb + fb_off;
             fb_off += (size_t)((L.npw + 7) / 8) * ((L.nph + 7) / 8);
@@ -1632,19 +1494,5 @@ dis_status dis_flow_color(const float* flow, int n, int width, int height, float
     hipFree(maxbits);
     return rc;
 }
-
-#ifdef DIS_STAMP
-// diagnostic builds only (not in include/dis_abi.h): copy the stamp buffer
-int dis_stamp_read(dis_ctx* c, unsigned long long* host, size_t n)
-{
-    if (!c || !c->stamp || !host) return -1;
-    hipSetDevice(c->device);
-    const size_t ns = (size_t)dis_ctx::kMaxSub * (1 + 2 * dis::kStampN);
-    return hipMemcpy(host, c->stamp, sizeof(unsigned long long) * std::min(n, ns), hipMemcpyDeviceToHost) ==
-                   hipSuccess
-               ? 0
-               : -1;
-}
-#endif
 
 }  // extern "C"

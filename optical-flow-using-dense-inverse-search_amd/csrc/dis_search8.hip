@@ -39,58 +39,6 @@
 #include "dis_device.h"
 #include "dis_kernels.h"
 
-#ifndef DIS_SOBEL_FENCE
-#define DIS_SOBEL_FENCE __builtin_amdgcn_sched_barrier(0)  // rows streamed: bounded VGPRs
-#endif
-#ifndef DIS_S8_EXTRA_ATTR
-#define DIS_S8_EXTRA_ATTR
-#endif
-#ifndef DIS_LOOP_SELECT
-#define DIS_LOOP_SELECT 1
-#endif
-#ifndef DIS_SPLIT_PATCH
-#define DIS_SPLIT_PATCH 1  // LPP 2: per-patch scalar work split between the patch's two lanes
-#endif
-#ifndef DIS_SPLIT_FENCE
-#define DIS_SPLIT_FENCE false  // sched fence per tap row: 124 VGPRs, measured -1.2 % (r03 A/B)
-#endif
-#ifndef DIS_TAP_PREFETCH
-#define DIS_TAP_PREFETCH 0  // LPP 2 tile path: next update's taps read during the solve (iterate_split)
-#endif
-#ifndef DIS_TAP_PREFETCH_FMA
-#define DIS_TAP_PREFETCH_FMA DIS_TAP_PREFETCH  // the same for the tolerance-mode (kFma) kernels
-#endif
-#ifndef DIS_TAP_PREFETCH_ROWS
-#define DIS_TAP_PREFETCH_ROWS 3
-#endif
-#ifndef DIS_RHS_ORDER
-#define DIS_RHS_ORDER 1  // iterate_split: lanes carry the pivoted right-hand sides (no per-update swap selects)
-#endif
-#ifndef DIS_TAP_ADDR2
-#define DIS_TAP_ADDR2 1  // iterate_split tile path, tolerance mode: byte-offset tap bases, VGPR row step
-#endif
-#ifndef DIS_TAP_ADDR3
-#define DIS_TAP_ADDR3 1  // the same byte offsets in the exact kernel, row-group bases added per update
-#endif
-#ifndef DIS_RESET_OUT
-#define DIS_RESET_OUT 1  // iterate_split: the outlier reset applied once, after the loop, on the exiting lanes
-#endif
-#ifndef DIS_FMA_CENTER
-#define DIS_FMA_CENTER 1  // tolerance mode: centred template gradients instead of a per-update mean (see search_block)
-#endif
-#ifndef DIS_FMA_FUSED
-#define DIS_FMA_FUSED 1  // tolerance mode, LPP 2: warp fused into the dot products (iterate_split)
-#endif
-#ifndef DIS_FMA_FENCE
-#define DIS_FMA_FENCE 1  // fused loop: taps streamed row by row (109 VGPRs instead of 128 + a spill; r04 A/B 1.015 vs 1.031 ms)
-#endif
-#ifndef DIS_FMA_WAVES
-#define DIS_FMA_WAVES 4  // min waves per SIMD of the tolerance-mode LPP-2 tile kernel
-#endif
-#ifndef DIS_SEARCH8_WAVES
-#define DIS_SEARCH8_WAVES 5  // min waves per SIMD (caps VGPRs at 96; measured +1% over 4)
-#endif
-
 namespace dis {
 
 namespace {
@@ -101,38 +49,19 @@ constexpr int kBX = LPP == 1 ? 16 : 8;
 constexpr int kBY = 8;
 template <int LPP>
 constexpr int kThreads = kBX<LPP> * kBY * LPP;
-#ifndef DIS_TILE_H
-#define DIS_TILE_H 64
-#endif
-constexpr int kTileH = DIS_TILE_H;  // max staged tile rows
+constexpr int kTileH = 64;  // max staged tile rows
 template <int LPP>
 constexpr int kTileW = LPP == 1 ? 96 : 64;  // max staged tile columns
-#ifndef DIS_TSMAX2
-#define DIS_TSMAX2 72  // 64 x 72-float tile (18 KB): 8 two-wave workgroups per CU = 4 waves per SIMD at LPP 2
-#endif
+// max tile row stride (floats); the host picks it per grid step. LPP 2: a
+// 64 x 72-float tile (18 KB): 8 two-wave workgroups per CU = 4 waves per SIMD
 template <int LPP>
-constexpr int kTSMax = LPP == 1 ? 128 : DIS_TSMAX2;  // max tile row stride (floats); the host picks it per grid step
+constexpr int kTSMax = LPP == 1 ? 128 : 72;
 template <int LPP>
 constexpr int kCuMax = LPP == 1 ? 192 : 144;  // staged coarse patches (<= 16 x 12 / 12 x 12 for steps >= 1)
 template <int LPP>
 constexpr int kCuPer = (kCuMax<LPP> + kThreads<LPP> - 1) / kThreads<LPP>;  // coarse patches per thread
-#ifndef DIS_FB_LPP8
-// 1: exact modes search the LPP-2 lists at 8 lanes per patch (no spill; 2.3x
-// faster when most blocks are listed, variant 9) -- off: its 8-wave workgroups
-// wait for slots beside the other sub-batch's search, and the usually empty
-// launch then costs the step 1 % (r04 A/B)
-#define DIS_FB_LPP8 0
-#endif
-#ifndef DIS_FB_MERGED_WGS
-#define DIS_FB_MERGED_WGS 256  // fallback workers appended to a merged launch
-#endif
-#ifndef DIS_FB_WGS
-#define DIS_FB_WGS 256
-#endif
-#ifndef DIS_TILE_GROUP
-#define DIS_TILE_GROUP 8
-#endif
-constexpr int kTileGroup = DIS_TILE_GROUP;  // tile rows per wave in flight
+constexpr int kFbWgs = 256;    // persistent k_search8_fb workgroups (grid-stride over the list)
+constexpr int kTileGroup = 8;  // tile rows per wave in flight
 
 // quad_perm DPP controls
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
@@ -284,29 +213,9 @@ __device__ __forceinline__ int wave_max(int v)
 }
 
 // Bilinear warp + mean normalisation (src/patch.cpp:207-267) for one patch
-// position; `tap(row, col)` returns the target image at (Y-5+row, X-5+q+col)
-// relative rows 0..8 and relative cols {0,1} (set 0) / {4,5} (set 1).
-struct Warp {
-    float w0, w1, w2, w3;
-    int X, Y;
-};
-
-__device__ __forceinline__ Warp warp_coefs(float x, float y)
-{
-    Warp w;
-    const float l = floorf(x), k = floorf(y);
-    const float a = x - l, b = y - k;
-    w.w0 = (1 - a) * (1 - b);
-    w.w1 = a * (1 - b);
-    w.w2 = b * (1 - a);
-    w.w3 = a * b;
-    w.X = (int)ceilf(x + .00001f);  // Q8: the epsilon is a no-op from 256 on
-    w.Y = (int)ceilf(y + .00001f);
-    return w;
-}
-
-// `tap(k, c)` returns the target image at row Y-5+k (k = 0..8) and column
-// X-5 + qb + c, qb = the lane's first pixel column (LPP 1: 0, LPP 2: 4q, else q).
+// position (warp_coefs, dis_device.h). `tap(k, c)` returns the target image at
+// row Y-5+k (k = 0..8) and column X-5 + qb + c, qb = the lane's first pixel
+// column (LPP 1: 0, LPP 2: 4q, else q).
 template <int LPP, bool kFence = false, bool kFma = false, typename Tap>
 __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, float (&r)[8 * kNCol<LPP>])
 {
@@ -354,7 +263,7 @@ __device__ __forceinline__ void warp_patch(const Warp& w, int norm, Tap&& tap, f
         }
     }
     // (tolerance mode: the mean is folded into centred gradients, search_block)
-    if (norm && !(kFma && DIS_FMA_CENTER)) {
+    if (norm && !kFma) {
         // sum / num_points_patch (:265); x / 64 = x * 2^-6 exactly rounded either
         // way, as v_ldexp (inline exponent) instead of a v_mul with a literal
         const float mean = __builtin_amdgcn_ldexpf(patch_sum<LPP>(r), -6);
@@ -409,28 +318,13 @@ __device__ __forceinline__ void iterate(const Search8Args& a, const LU2& lu, con
         const float ex = sx - px, ey = sy - py;
         const float s2 = ex * ex + ey * ey;
         // sqrtf(s2) > outlierthresh  <=>  s2 > thr_sq (sqrt is correctly rounded
-        // and monotone; thr_sq precomputed on the host); NaN -> reset (see oracle)
-#if DIS_LOOP_SELECT
-        // one exit test: the reset as selects, then a single divergent break
+        // and monotone; thr_sq precomputed on the host); NaN -> reset (see oracle).
+        // One exit test: the reset as selects, then a single divergent break.
         const bool bad = s2 > a.thr_sq || s2 != s2 || px < a.tmp_lb || py < a.tmp_lb || px > a.tmp_ub_w ||
                          py > a.tmp_ub_h;
         u0 = bad ? ix : u0;
         u1 = bad ? iy : u1;
         if (bad || counter > a.iters) break;
-#else
-        if (s2 > a.thr_sq || s2 != s2 || px < a.tmp_lb || py < a.tmp_lb || px > a.tmp_ub_w ||
-            py > a.tmp_ub_h) {
-            u0 = ix;
-            u1 = iy;
-#ifdef DIS_EXP_FULLITERS  // experiment: reset and keep iterating (fixed work per patch)
-            px = sx;
-            py = sy;
-#else
-            break;
-#endif
-        }
-        if (counter > a.iters) break;
-#endif
     }
     *pu0 = u0;
     *pu1 = u1;
@@ -447,54 +341,26 @@ constexpr int kQuadOdd = 0xF5;   // [1,1,3,3]: lanes 2k, 2k+1 read lane 2k+1
 // position, its floor / fraction / ceil in the warp, its part of the tap base,
 // its displacement and its bounds test -- so one instruction serves both
 // coordinates, and the two right-hand sides come out one per lane from a
-// single cross-lane stage: lane 0 holds (g1, g2) = (gx, gy), lane 1 (gy, gx),
-// so C_ci = A_ci(g1) + partner's A_ci(g2) is b0's column sum on lane 0 and
-// b1's on lane 1. Every value is the one iterate() computes: the cross-lane
-// products and sums pair the same operands (IEEE mul and add commute), the
-// solve runs on both lanes from the same (c0, c1). `tap_at(cv)` gets the lane's
-// own ceil coordinate.
-//
-// kPrefetch (the LDS-tile path): the 45 taps of the next update are read from
-// LDS while this update's solve runs, at this update's tap base; the next
-// update re-reads them only if some lane's base moved (ceil(p + 1e-5) changed:
-// after the first few updates in ~8 % of wave-iterations at the finest 1080p
-// level), so the LDS latency no longer stalls the top of every update. The
-// tile is read-only during the loop: same values either way.
-template <bool kFence, bool kPaper, bool kFma, bool kPrefetch = false, typename TapAt>
+// single cross-lane stage. The caller arranged (g1, g2) so that lane 2k's own
+// sum is the pivoted c0 and lane 2k+1's c1 (PartialPivLU's row swap folded
+// into which gradient each lane carries): C_ci = A_ci(g1) + partner's A_ci(g2).
+// Every value is the one iterate() computes: the cross-lane products and sums
+// pair the same operands (IEEE mul and add commute), the solve runs on both
+// lanes from the same (c0, c1). `tap_at(cv)` gets the lane's own ceil
+// coordinate. The outlier reset is applied once, after the loop, on the
+// exiting lanes.
+template <bool kFence, bool kPaper, bool kFma, typename TapAt>
 __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& lu, const float (&g1)[32],
                                               const float (&g2)[32], int q, float rv, float iv, float btv,
                                               float* puv, TapAt&& tap_at)
 {
-    auto mac = [](float acc, float x, float y) { return kFma ? __builtin_fmaf(x, y, acc) : acc + x * y; };
-    constexpr bool kFused = kFma && DIS_FMA_CENTER && DIS_FMA_FUSED && !kPrefetch;
     float uv = iv;
     const float sv = rv + uv;
     float pv = sv;
-    bool reset = false;  // DIS_RESET_OUT: the exit was an outlier / out-of-bounds reset
+    bool reset = false;  // the exit was an outlier / out-of-bounds reset
     const float ubv = q ? a.tmp_ub_h : a.tmp_ub_w;
-    // DIS_RHS_ORDER: the caller arranged (g1, g2) so that lane 2k's own sum is
-    // the pivoted c0 and lane 2k+1's c1 (PartialPivLU's row swap folded into
-    // which gradient each lane carries); otherwise lane q's own sum is b_q and
-    // c0 takes the partner's when f
-    const bool f = (lu.swap != 0) != (q != 0);
     float r[32];
     const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;  // div_pre
-    constexpr int PR = DIS_TAP_PREFETCH_ROWS;  // tap rows read ahead (the rest stream behind them)
-    float T[kPrefetch ? PR : 1][5];
-    int cvl = 0;  // the lane's coordinate of the base T was read at
-    auto load_taps = [&](int cvv) {
-        if constexpr (kPrefetch) {
-            auto tap = tap_at(cvv);
-#pragma unroll
-            for (int k = 0; k < PR; ++k)
-#pragma unroll
-                for (int c = 0; c < 5; ++c) T[k][c] = tap(k, c);
-        }
-    };
-    if constexpr (kPrefetch) {
-        cvl = (int)ceilf(pv + .00001f);
-        load_taps(cvl);
-    }
     for (int counter = 1;; ++counter) {
         // warp_coefs, one coordinate per lane: a (b) = frac, 1 - a (1 - b)
         const float fl = floorf(pv), fr = pv - fl, om = 1 - fr;
@@ -505,29 +371,13 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         w.w1 = xor1f(s1) * s1;    // a (1 - b)
         w.w2 = xor1f(s2w) * s2w;  // b (1 - a)
         w.w3 = xor1f(fr) * fr;    // a b
-        if constexpr (kPrefetch) {
-            // a pair whose base moved reads at the new one (exec-masked: no
-            // wave-uniform branch, so the read-ahead rows keep their registers)
-            // (both DPP reads before any branch: a short-circuit || would run
-            // the second pair under a divergent mask and read disabled lanes)
-            const int pcv = xor1i(cv), pcvl = xor1i(cvl);
-            const bool moved = (cv != cvl) | (pcv != pcvl);
-            if (moved) {
-                cvl = cv;
-                load_taps(cvl);
-            }
-            auto tap = tap_at(cvl);
-            warp_patch<2, kFence, kFma>(w, a.norm, [&](int k, int c) { return k < PR ? T[k < PR ? k : 0][c] : tap(k, c); },
-                                        r);
-        } else if constexpr (!kFused) {
-            warp_patch<2, kFence, kFma>(w, a.norm, tap_at(cv), r);
-        }
-        float bown;  // lane 2k: its own right-hand side, 2k+1: its own
-        if constexpr (kFused) {
+        float bown;               // lane 2k: the pivoted c0's sum, 2k+1: c1's
+        if constexpr (kFma) {
             // tolerance mode with centred gradients (no mean of the warped
             // patch): each warped pixel goes straight into the two dot products,
             // no residual array (fewer VGPRs), per-column accumulators summed
-            // in-lane, one cross-lane add per right-hand side
+            // in-lane, one cross-lane add per right-hand side; taps streamed
+            // row by row (109 VGPRs instead of 128 + a spill)
             auto tap = tap_at(cv);
             float x[4], y[4], prev[5], cur[5];
 #pragma unroll
@@ -547,51 +397,35 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
                 }
 #pragma unroll
                 for (int c = 0; c < 5; ++c) prev[c] = cur[c];
-                if constexpr (DIS_FMA_FENCE) __builtin_amdgcn_sched_barrier(0);  // taps streamed row by row
+                __builtin_amdgcn_sched_barrier(0);
             }
             bown = ((x[0] + x[1]) + (x[2] + x[3])) + xor1f((y[0] + y[1]) + (y[2] + y[3]));
         } else {
+            warp_patch<2, kFence, false>(w, a.norm, tap_at(cv), r);
             float C[4];
 #pragma unroll
             for (int ci = 0; ci < 4; ++ci) {
                 float x = g1[8 * ci] * r[8 * ci], y = g2[8 * ci] * r[8 * ci];
 #pragma unroll
                 for (int j = 1; j < 8; ++j) {
-                    x = mac(x, g1[8 * ci + j], r[8 * ci + j]);
-                    y = mac(y, g2[8 * ci + j], r[8 * ci + j]);
+                    x = x + g1[8 * ci + j] * r[8 * ci + j];
+                    y = y + g2[8 * ci + j] * r[8 * ci + j];
                 }
                 C[ci] = x + xor1f(y);
             }
-            bown = (C[0] + C[2]) + (C[1] + C[3]);  // lane 0: b0, lane 1: b1
+            bown = (C[0] + C[2]) + (C[1] + C[3]);
         }
         if constexpr (kPaper) bown = bown - btv;
-        const float bpart = xor1f(bown);
-        if constexpr (kPrefetch) {  // the next update's taps, in flight during the solve
-            load_taps(cvl);
-            __builtin_amdgcn_sched_barrier(0);
-        }
         float d0, c1;
         {  // lu2_solve (PartialPivLU::solve, src/patch.cpp:176) with div_pre
-            float c0;
-            if constexpr (DIS_RHS_ORDER) {
-                (void)bpart;
-                (void)f;
-                c0 = quad_perm<kQuadEven>(bown);                                      // lane 2k's sum
-                c1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bown), kQuadOdd, 0xF, 0xF, true)) -
-                     lu.l10 * c0;                                                    // lane 2k+1's
-            } else {
-                c0 = f ? bpart : bown;
-                c1 = f ? bown : bpart;
-                c1 = c1 - lu.l10 * c0;
-            }
-            if constexpr (kFma) {
+            const float c0 = quad_perm<kQuadEven>(bown);  // lane 2k's sum
+            c1 = quad_perm<kQuadOdd>(bown) - lu.l10 * c0;  // lane 2k+1's
+            if constexpr (kFma) {  // tolerance mode: multiply by the rounded reciprocal
                 c1 = c1 * r11;
-                c0 = __builtin_fmaf(-c1, lu.u01, c0);
-                d0 = c0 * r00;
+                d0 = __builtin_fmaf(-c1, lu.u01, c0) * r00;
             } else {
                 c1 = div_pre(c1, lu.u11, r11);
-                c0 = c0 - c1 * lu.u01;
-                d0 = div_pre(c0, lu.u00, r00);
+                d0 = div_pre(c0 - c1 * lu.u01, lu.u00, r00);
             }
         }
         uv = uv - (q ? c1 : d0);
@@ -599,43 +433,27 @@ __device__ __forceinline__ void iterate_split(const Search8Args& a, const LU2& l
         const float ev = sv - pv, e2 = ev * ev;
         const float n2 = e2 + xor1f(e2);  // ex * ex + ey * ey
         // either coordinate out: the pair's OR, on the scalar unit (one ballot
-        // per compare: each v_cmp writes its lane mask straight to SGPRs)
+        // per compare: each v_cmp writes its lane mask straight to SGPRs);
         // !(n2 <= thr_sq): over the threshold or NaN in one compare
         unsigned long long m = __builtin_amdgcn_ballot_w64(!(n2 <= a.thr_sq)) |
                                __builtin_amdgcn_ballot_w64(pv < a.tmp_lb) | __builtin_amdgcn_ballot_w64(pv > ubv);
         m |= ((m >> 1) & 0x5555555555555555ull) | ((m << 1) & 0xAAAAAAAAAAAAAAAAull);
         const bool bad = __builtin_amdgcn_inverse_ballot_w64(m);
-#if DIS_RESET_OUT
-        // the reset (u = the initial u, src/patch.cpp:190) on the exiting lanes
-        // only, after the loop: no select per update
         if (bad || counter > a.iters) {
             reset = bad;
             break;
         }
-#else
-        uv = bad ? iv : uv;
-        if (bad || counter > a.iters) break;
-#endif
     }
     *puv = reset ? iv : uv;
 }
 
 }  // namespace
 
-#ifndef DIS_XCD_REMAP
-#define DIS_XCD_REMAP 1
-#endif
-#ifndef DIS_FB_WAVES
-#define DIS_FB_WAVES 3
-#endif
-#ifndef DIS_SPLIT_FB
-#define DIS_SPLIT_FB 1
-#endif
-#ifndef DIS_EXP_NO_FB
-#define DIS_EXP_NO_FB 0  // experiment: no k_search8_fb launches (wrong values if a list is not empty)
-#endif
-template <int LPP, bool kFallback, bool kFma = false>
-constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? DIS_FB_WAVES : kFma ? DIS_FMA_WAVES : 4) : DIS_SEARCH8_WAVES;  // min waves per SIMD
+// min waves per SIMD: LPP 1 holds 192 VGPRs of gradients and warp; the LPP-2
+// tile kernel 128 (4 per SIMD, also the LDS tile's limit); its fallback form
+// 3; LPP 4 / 8 are capped at 96 VGPRs (5 per SIMD: measured +1 % over 4)
+template <int LPP, bool kFallback>
+constexpr int kWaves = LPP == 1 ? 2 : LPP == 2 ? (kFallback ? 3 : 4) : 5;
 
 // LDS of one workgroup (block of patches)
 template <int LPP>
@@ -660,13 +478,7 @@ struct BlockLds {
 // TSC: the LDS tile row stride as a compile-time constant (0: a.tile_stride at
 // run time). Constant, all 45 taps of an update come from one base address
 // plus ds_read immediate offsets (no per-row address arithmetic).
-// kXcd (k_search8_head): the coarser level's patch displacements were written
-// by other workgroups of the same launch, possibly on other XCDs, whose L2s
-// are not coherent: they are read, and this level's are written, as
-// agent-scope atomics (global_load / global_store sc1), so no L2 write-back
-// or invalidation fence is needed.
-template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false, int TSC = 0,
-          bool kXcd = false>
+template <int LPP, bool kFallback, bool kPaper, bool kFma = false, bool kPhys = false, int TSC = 0>
 __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int byi, int pair, BlockLds<LPP>& S)
 {
     constexpr int NT = kThreads<LPP>, NW = NT / 64, NC = kNCol<LPP>, BX = kBX<LPP>;
@@ -725,15 +537,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         for (int k = 0; k < kCuPer<LPP>; ++k) {
             const int i = tid + k * NT;
             const int cx = floordiv_r(i, rph), cy = i - cx * PH;
-            if constexpr (kXcd) {
-                unsigned long long v = 0;
-                if (i < PN)
-                    v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(uc + (ga + cx) * a.c_nph + ha + cy),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cuv[k] = __builtin_bit_cast(float2, v);
-            } else {
-                cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
-            }
+            cuv[k] = i < PN ? uc[(ga + cx) * a.c_nph + ha + cy] : make_float2(0.0f, 0.0f);
         }
         if (tid < BX + kBY) {
             // covering coarse-patch range per block column / row (src/patch_grid.cpp:121-182
@@ -764,12 +568,8 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int r = r0 + NW * j;
-#ifdef DIS_EXP_NOREGIONLOAD  // experiment: no HBM reads of the I0 region (wrong values)
-                    v[j] = (float)(((r * 37) ^ (c0 * 11)) & 63);
-#else
                     v[j] = (r < RH && col < RW) ? I0[(size_t)clampi(reflect101(y0 + r, H), 0, H - 1) * W + c0]
                                                 : 0.0f;
-#endif
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -830,7 +630,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             row(j + 2);
-            DIS_SOBEL_FENCE;
+            __builtin_amdgcn_sched_barrier(0);  // rows streamed: bounded VGPRs
             const int py = iry - 4 + j;
 #pragma unroll
             for (int ci = 0; ci < NC; ++ci) {
@@ -907,7 +707,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         const float h11 = patch_dot<LPP, kFma>(gdy, [&](int j) { return gdy[j]; });
         lu = hessian_lu2(h00, h01, h11);
     }
-    if constexpr (kFma && DIS_FMA_CENTER) {
+    if constexpr (kFma) {
         // tolerance mode (summation order free within the stated tolerance):
         // sum(g (r - mean r)) = sum((g - mean g) r), so the right-hand sides
         // take gradients centred once per patch and the update loop skips the
@@ -922,11 +722,11 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             }
         }
     }
-    // LPP 2, split iteration (iterate_split): the y lane keeps (gy, gx)
-    constexpr bool kSplit = LPP == 2 && DIS_SPLIT_PATCH && !kPhys;
-    // (DIS_RHS_ORDER: the lane whose right-hand side is b1 -- the y lane, or
-    // the x lane when the LU pivot swapped the rows -- keeps (gy, gx))
-    [[maybe_unused]] const bool own_y = DIS_RHS_ORDER ? (lu.swap != 0) != (q != 0) : q != 0;
+    // LPP 2, split iteration (iterate_split): the lane whose right-hand side is
+    // b1 -- the y lane, or the x lane when the LU pivot swapped the rows --
+    // keeps (gy, gx)
+    constexpr bool kSplit = LPP == 2 && !kPhys;
+    [[maybe_unused]] const bool own_y = (lu.swap != 0) != (q != 0);
     if constexpr (kSplit) {
 #pragma unroll
         for (int j = 0; j < 8 * NC; ++j) {
@@ -965,23 +765,6 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int caph = a.tile_cap > 0 ? min(a.tile_cap, kTileH) : kTileH;
     const bool use_tile = any_valid && tw <= capw && th <= caph;
     const int TS = TSC ? TSC : a.tile_stride;  // rows of vertically adjacent patches on disjoint banks
-    if constexpr (DIS_FB_MERGED && LPP == 2 && !kFallback && !kPhys) {
-        // fallback workers in this launch (k_search8, a.fb_decided): list the
-        // block if it is too spread, then count this block's verdict. The entry
-        // is an agent-scope store acknowledged before the count (the workers may
-        // run on another XCD, whose L2 does not see this one's)
-        if (a.fb_decided && tid == 0) {
-            if (!use_tile && any_valid) {
-                const int slot = atomicAdd(a.fb_count, 1);
-                __hip_atomic_store(a.fb_list + slot, (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __hip_atomic_fetch_add(a.fb_decided + ((int)blockIdx.x % kFbSlots) * kFbSlotStride, 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-
     float u0 = ix, u1 = iy;
     float uv = q ? iy : ix;  // split iteration: the lane's coordinate
     if (use_tile) {
@@ -995,11 +778,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
                     const int r = r0 + NW * j;
-#ifdef DIS_EXP_NOTILELOAD  // experiment: no HBM reads of the I1 tile (wrong values)
-                    v[j] = (float)(((r * 37) ^ (cx * 11)) & 63);
-#else
                     v[j] = (r < th && col < tw) ? I1[(ptrdiff_t)clampi(ty0 + r, lo, H - 1 + pad) * ld + cx] : 0.0f;
-#endif
                 }
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
@@ -1015,80 +794,40 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // x lane (X - 5 - tx0), y lane (Y - 5 - ty0) TS; summed with the
                 // partner's by one DPP add
                 const int M = q ? TS : 1, K = q ? -(5 + ty0) * TS : -(5 + tx0);
-                const float* tq = tile + 4 * q;
-#if DIS_TAP_ADDR2
-                // (kFma) byte offsets: t = cv * 4M + 4K, the pair's sum by one DPP
-                // add, the three row-group bases (ds_read2 immediates <= 255
-                // dwords) by adding a VGPR-held 3-row step: 5 address VALU per
-                // update instead of 7, no literal operands
+                // byte offsets: t = cv * 4M + 4K, the pair's sum by one DPP add,
+                // then three row-group bases (ds_read2 immediates <= 255 dwords)
                 const int M4 = 4 * M, K4 = 4 * K;
-                const char* const tqb = reinterpret_cast<const char*>(tq);
-                // three rows, in bytes: a loop-invariant VGPR operand instead of a
-                // literal (tolerance mode only: the exact kernel is at 128 VGPRs
-                // and spilled; with literals its loop grew 463 -> 470 VALU)
+                typedef __attribute__((address_space(3))) const char* lds_cp;
+                typedef __attribute__((address_space(3))) const float* lds_fp;
+                const lds_cp tqb = (lds_cp)(tile + 4 * q);
+                // tolerance mode: the three-row step as a loop-invariant VGPR
+                // operand (5 address VALU per update instead of 7); the exact
+                // kernel is at 128 VGPRs and spilled with it, so it adds the two
+                // further bases per update behind opaque copies (a literal each)
                 int g3 = 12 * TS;
                 if constexpr (kFma) __asm__("" : "+v"(g3));
-#endif
-                iterate_split<DIS_SPLIT_FENCE, kPaper, kFma, (kFma ? DIS_TAP_PREFETCH_FMA : DIS_TAP_PREFETCH) != 0>(
-                                                                             a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix,
-                                                                             own_y ? bt1 : bt0, &uv,
-                                                   [&](int cv) {
-#if DIS_TAP_ADDR2
-                                                     if constexpr (kFma) {
+                iterate_split<false, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, own_y ? bt1 : bt0,
+                                                   &uv, [&](int cv) {
                                                        const int tb = __mul24(cv, M4) + K4;
-                                                       const char* const c0 = tqb + (tb + xor1i(tb));
-                                                       const float *f0 = reinterpret_cast<const float*>(c0),
-                                                                   *f1 = reinterpret_cast<const float*>(c0 + g3),
-                                                                   *f2 = reinterpret_cast<const float*>(c0 + g3 + g3);
-                                                       return [=](int k, int c) {
-                                                           return k < 3 ? f0[k * TS + c]
-                                                                        : k < 6 ? f1[(k - 3) * TS + c] : f2[(k - 6) * TS + c];
-                                                       };
-                                                     } else if constexpr (DIS_TAP_ADDR3) {
-                                                       // exact kernel: byte offsets too, the two further row-group
-                                                       // bases added per update behind opaque copies (a literal each;
-                                                       // no VGPR held across the loop)
-                                                       typedef __attribute__((address_space(3))) const char* lds_cp;
-                                                       typedef __attribute__((address_space(3))) const float* lds_fp;
-                                                       const int tb = __mul24(cv, M4) + K4;
-                                                       lds_cp c0 = (lds_cp)tqb + (tb + xor1i(tb));
-                                                       lds_cp c1 = c0 + 12 * TS;
-                                                       lds_cp c2 = c0 + 24 * TS;
-                                                       __asm__("" : "+v"(c1));
-                                                       __asm__("" : "+v"(c2));
+                                                       const lds_cp c0 = tqb + (tb + xor1i(tb));
+                                                       lds_cp c1 = c0 + g3, c2 = c1 + g3;
+                                                       if constexpr (!kFma) {
+                                                           c1 = c0 + 12 * TS;
+                                                           c2 = c0 + 24 * TS;
+                                                           __asm__("" : "+v"(c1));
+                                                           __asm__("" : "+v"(c2));
+                                                       }
                                                        const lds_fp f0 = (lds_fp)c0, f1 = (lds_fp)c1, f2 = (lds_fp)c2;
                                                        return [=](int k, int c) {
                                                            return k < 3 ? f0[k * TS + c]
                                                                         : k < 6 ? f1[(k - 3) * TS + c] : f2[(k - 6) * TS + c];
                                                        };
-                                                     } else {
-#endif
-                                                       const int t = __mul24(cv, M) + K;
-                                                       // three row groups, each one base register and
-                                                       // ds_read2 immediates (<= 255 dwords); opaque to the
-                                                       // compiler, which otherwise re-adds a base per pair
-                                                       const int o0 = t + xor1i(t);
-                                                       int o1 = o0 + 3 * TS, o2 = o0 + 6 * TS;
-                                                       __asm__("" : "+v"(o1));
-                                                       __asm__("" : "+v"(o2));
-                                                       const float *b0 = tq + o0, *b1 = tq + o1, *b2 = tq + o2;
-                                                       return [=](int k, int c) {
-                                                           return k < 3 ? b0[k * TS + c]
-                                                                        : k < 6 ? b1[(k - 3) * TS + c] : b2[(k - 6) * TS + c];
-                                                       };
-#if DIS_TAP_ADDR2
-                                                     }
-#endif
                                                    });
             }
         } else if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;  // lane's first tap column
             iterate<LPP, false, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
-#ifdef DIS_EXP_TAPBANKS  // experiment: lane-fixed, conflict-free tap addresses (wrong values)
-                const float* base = tile + (lane & 31) + ((w.X & 1) << 5) + 0 * qb;
-#else
                 const float* base = tile + (w.Y - 5 - ty0) * TS + (w.X - 5 + qb - tx0);
-#endif
                 return [=](int k, int c) { return base[k * TS + c]; };
             });
         }
@@ -1115,9 +854,8 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             });
         }
     } else if (any_valid) {
-        // too spread for the tile: k_search8_fb (or this launch's fallback
-        // workers, listed above) redoes this block
-        if (tid == 0 && !a.fb_decided) {
+        // too spread for the tile: k_search8_fb redoes this block
+        if (tid == 0) {
             const int slot = atomicAdd(a.fb_count, 1);
             a.fb_list[slot] = (pair * ((a.nph + kBY - 1) / kBY) + byi) * ((a.npw + BX - 1) / BX) + bxi;
         }
@@ -1129,201 +867,16 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         u1 = q ? uv : up;
     }
     if (active && q == 0) {
-        float2* const o = a.u_out + (size_t)pair * a.u_stride + gx * a.nph + gy;
-        if constexpr (kXcd)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(o),
-                               __builtin_bit_cast(unsigned long long, make_float2(u0, u1)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        else
-            *o = make_float2(u0, u1);
+        a.u_out[(size_t)pair * a.u_stride + gx * a.nph + gy] = make_float2(u0, u1);
     }
-}
-
-// ---------------------------------------------------------------------------
-// LPP 64: the north star's mapping -- one wave64 per 8x8 patch, lane = pixel
-// (column c = lane / 8, row j = lane % 8), the patch's 21 x 21 target window
-// staged in LDS, the reductions across lanes. Eigen's order (A_c = sequential
-// sum down column c, then ((A0+A4)+(A2+A6))+((A1+A5)+(A3+A7))) makes each
-// reduction a 7-step dependent chain across the column's lanes (DPP row_shr:1)
-// plus 8 readlanes: ~30 instructions per sum, three sums per update, for ONE
-// patch per wave -- ~150 wave instructions per patch-update against ~16 at
-// LPP 2. Kept as a measured variant (dis_set_kernel_variant 6).
-namespace {
-
-constexpr int kWaveWin = 21;  // window rows / columns: floor(start) -10 .. +10
-
-__device__ __forceinline__ float row_shr1(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));  // row_shr:1
-}
-
-// Eigen-order sum over the wave's 64 lanes (lane = 8 c + j holds pixel (j, c));
-// the result is wave-uniform
-__device__ __forceinline__ float wave_patch_sum(float v, int j)
-{
-    float s = v;
-#pragma unroll
-    for (int k = 1; k < 8; ++k) {
-        const float t = row_shr1(s) + v;  // lane j: S_{j-1} + v_j
-        s = j == k ? t : s;
-    }
-    float A[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) A[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 8 * c + 7));
-    return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
-}
-
-}  // namespace
-
-// grid: (ceil(npw * nph / 4), batch), 4 waves (patches) per workgroup, exact
-// arithmetic only (the runtime uses it for exact, non-paper, virtual-padding
-// levels; the compat and tolerance paths keep their kernels)
-__global__ void __launch_bounds__(256) k_search_wave(Search8Args a)
-{
-    __shared__ float win_all[4][kWaveWin * kWaveWin];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int p = blockIdx.x * 4 + wave;  // patch id, x-major (src/patch_grid.cpp:39-50)
-    const int pair = blockIdx.y;
-    if (p >= a.npw * a.nph) return;  // whole wave; no workgroup barrier below
-    float* const win = win_all[wave];
-    const int gx = p / a.nph, gy = p - gx * a.nph;
-    const int st = a.steps, W = a.W, H = a.H;
-    const int irx = gx * st + a.offw, iry = gy * st + a.offh;
-    const float rx = (float)irx, ry = (float)iry;
-    const int c = lane >> 3, j = lane & 7;
-    const float* I0 = a.img0 + (size_t)pair * a.plane_stride + a.plane_off;
-    const float* I1 = a.img1 + (size_t)pair * a.plane_stride + a.plane_off;
-
-    // template gradients at pixel (irx-4+c, iry-4+j): Sobel (ksize 3, 1/8,
-    // reflect-101) of the level image, zero outside it (src/main.cpp:34-47)
-    const int px = irx - 4 + c, py = iry - 4 + j;
-    float R[3], S[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float* row = I0 + (size_t)clampi(reflect101(py - 1 + k, H), 0, H - 1) * W;
-        const float l = row[clampi(reflect101(px - 1, W), 0, W - 1)];
-        const float m = row[clampi(reflect101(px, W), 0, W - 1)];
-        const float r = row[clampi(reflect101(px + 1, W), 0, W - 1)];
-        R[k] = r - l;
-        S[k] = m * 0.25f + (l + r) * 0.125f;
-    }
-    const bool in = px >= 0 && px < W && py >= 0 && py < H;
-    const float gdx = in ? R[1] * 0.25f + (R[0] + R[2]) * 0.125f : 0.0f;
-    const float gdy = in ? S[2] - S[0] : 0.0f;
-    const LU2 lu = hessian_lu2(wave_patch_sum(gdx * gdx, j), wave_patch_sum(gdx * gdy, j),
-                               wave_patch_sum(gdy * gdy, j));
-
-    // initialisation from the coarser level (src/patch_grid.cpp:108-119)
-    float ix = 0.0f, iy = 0.0f;
-    if (a.u_init) {
-        const float2 v = a.u_init[(size_t)pair * a.init_stride + p];
-        ix = v.x;
-        iy = v.y;
-    } else if (a.dense_coarse) {
-        const float2 d = a.dense_coarse[(size_t)pair * a.dense_stride + (size_t)(iry >> 1) * (W / 2) + (irx >> 1)];
-        ix = d.x * 2;
-        iy = d.y * 2;
-    } else if (a.u_coarse) {
-        const float2 d = dense_at(a.u_coarse + (size_t)pair * a.u_stride, a.c_npw, a.c_nph, a.c_offw, a.c_offh, st, 4,
-                                  irx >> 1, iry >> 1);
-        ix = d.x * 2;
-        iy = d.y * 2;
-    }
-    const float sx = rx + ix, sy = ry + iy;
-    float u0 = ix, u1 = iy;
-    if (!(sx < a.tmp_lb || sy < a.tmp_lb || sx > a.tmp_ub_w || sy > a.tmp_ub_h)) {
-        // the patch's window: every tap lies in floor(start) -9 .. +9 (search_block 4)
-        const int tx0 = (int)floorf(sx) - 10, ty0 = (int)floorf(sy) - 10;
-        for (int i = lane; i < kWaveWin * kWaveWin; i += 64) {
-            const int r = i / kWaveWin, cc = i - r * kWaveWin;
-            win[i] = I1[(size_t)clampi(ty0 + r, 0, H - 1) * W + clampi(tx0 + cc, 0, W - 1)];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const float r00 = 1.0f / lu.u00, r11 = 1.0f / lu.u11;
-        float pxs = sx, pys = sy;
-        for (int counter = 1;; ++counter) {
-            const Warp w = warp_coefs(pxs, pys);
-            // pixel (j, c): A = (Y-4+j, X-4+c), B = A-1, C = A-row, D = C-1 (src/patch.cpp:247-261)
-            const float* b = win + (w.Y - 5 + j - ty0) * kWaveWin + (w.X - 5 + c - tx0);
-            float r = w.w3 * b[kWaveWin + 1];
-            r = r + w.w2 * b[kWaveWin];
-            r = r + w.w1 * b[1];
-            r = r + w.w0 * b[0];
-            if (a.norm) r = r - wave_patch_sum(r, j) / 64.0f;
-            const float b0 = wave_patch_sum(gdx * r, j), b1 = wave_patch_sum(gdy * r, j);
-            float c0 = lu.swap ? b1 : b0, c1 = lu.swap ? b0 : b1;
-            c1 = c1 - lu.l10 * c0;
-            c1 = div_pre(c1, lu.u11, r11);
-            c0 = c0 - c1 * lu.u01;
-            const float d0 = div_pre(c0, lu.u00, r00), d1 = c1;
-            u0 = u0 - d0;
-            u1 = u1 - d1;
-            pxs = rx + u0;
-            pys = ry + u1;
-            const float ex = sx - pxs, ey = sy - pys;
-            const float s2 = ex * ex + ey * ey;
-            if (s2 > a.thr_sq || s2 != s2 || pxs < a.tmp_lb || pys < a.tmp_lb || pxs > a.tmp_ub_w ||
-                pys > a.tmp_ub_h) {
-                u0 = ix;
-                u1 = iy;
-                break;
-            }
-            if (counter > a.iters) break;
-        }
-    }
-    if (lane == 0) a.u_out[(size_t)pair * a.u_stride + p] = make_float2(u0, u1);
 }
 
 // grid: (ceil(npw/kBX), ceil(nph/kBY), batch); one block of patches per workgroup
 template <int LPP, bool kFallback, bool kPaper = false, bool kFma = false, bool kPhys = false, int TSC = 0>
-__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback, kFma>)))
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, kFallback>)))
 k_search8(Search8Args a)
 {
     __shared__ BlockLds<LPP> S;
-    if constexpr (DIS_FB_MERGED && LPP == 2 && !kFallback && !kPhys) {
-        if (a.fb_decided) {
-            // 1-D grid: the level's blocks (XCD-remapped as below), then
-            // a.fb_wgs fallback workers. Workgroups are dispatched in id order,
-            // so every block workgroup is resident or done before a worker
-            // starts waiting for the verdict count; none of them waits on
-            // anything, so the count completes (the wait is bounded all the same)
-            const int nbx = (a.npw + kBX<LPP> - 1) / kBX<LPP>, nby = (a.nph + kBY - 1) / kBY;
-            const int nb = (int)gridDim.x - a.fb_wgs, lin = blockIdx.x;
-            if (lin >= nb) {
-                if (threadIdx.x == 0)
-                    for (int spin = 0; spin < (1 << 22); ++spin) {  // ~0.5 us per poll, at most ~2 s
-                        int sum = 0;
-#pragma unroll
-                        for (int k = 0; k < kFbSlots; ++k)
-                            sum += __hip_atomic_load(a.fb_decided + k * kFbSlotStride, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                        if (sum >= nb) break;
-                        __builtin_amdgcn_s_sleep(16);
-                    }
-                __syncthreads();
-                const int n = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(a.fb_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                for (int i = lin - nb; i < n; i += a.fb_wgs) {
-                    const int e = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load(a.fb_list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    const int bx = e % nbx, t = e / nbx;
-                    search_block<LPP, true, kPaper, kFma>(a, bx, t % nby, t / nby, S);
-                    __syncthreads();  // LDS reuse by the next listed block
-                }
-                return;
-            }
-            const int per = nb / 8;
-            const int t = DIS_XCD_REMAP && lin < per * 8 ? (lin % 8) * per + lin / 8 : lin;
-            const int bx = __builtin_amdgcn_readfirstlane(t % nbx);
-            const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
-            const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
-            search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, bx, by, bz, S);
-            return;
-        }
-    }
-#if DIS_XCD_REMAP
     // XCD-aware block order: the dispatcher deals linear workgroup ids
     // round-robin to the 8 XCDs; remap so each XCD walks a contiguous run of
     // blocks and neighbouring blocks' overlapping tiles (halo rows) are
@@ -1336,46 +889,6 @@ k_search8(Search8Args a)
     const int by = __builtin_amdgcn_readfirstlane((t / nbx) % nby);
     const int bz = __builtin_amdgcn_readfirstlane(t / (nbx * nby));
     search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, bx, by, bz, S);
-#else
-    search_block<LPP, kFallback, kPaper, kFma, kPhys, TSC>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
-#endif
-}
-
-// The coarse head in one launch (HeadArgs, dis_kernels.h): workgroup b runs
-// block (bx, by) of pair `pair` at head level i; level i > 0 first waits
-// until every block of the pair at level i - 1 has published its patch
-// displacements. The blocks run on any XCD: the displacements and counters
-// are agent-scope atomics (search_block kXcd), and a block counts itself done
-// only after its stores are acknowledged (vmcnt 0) -- no agent-scope
-// release/acquire fences, whose L2 write-back / invalidation (buffer_wbl2 /
-// buffer_inv sc1) cost the co-running sub-batch its L2 contents (r04: the
-// step 11 % slower with them). Deadlock-free with in-order workgroup
-// dispatch: a block waits only for blocks of lower workgroup ids, which were
-// dispatched before it and never wait on it.
-template <bool kFma, int TSC>
-__global__ void __launch_bounds__(kThreads<8>) __attribute__((amdgpu_waves_per_eu(kWaves<8, true>)))
-k_search8_head(HeadArgs h)
-{
-    __shared__ BlockLds<8> S;
-    const int b = blockIdx.x;
-    int i = 0;
-    while (i + 1 < h.nlev && b >= h.start[i + 1]) ++i;
-    const int per = h.nbx[i] * h.nby[i], local = b - h.start[i];
-    const int pair = local / per, blk = local - pair * per;
-    const int by = blk / h.nbx[i], bx = blk - by * h.nbx[i];
-    if (i > 0) {
-        if (threadIdx.x == 0) {
-            const int* d = h.done + (i - 1) * h.batch + pair;
-            const int need = h.nbx[i - 1] * h.nby[i - 1];
-            while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-                __builtin_amdgcn_s_sleep(1);
-        }
-        __syncthreads();
-    }
-    search_block<8, true, false, kFma, false, TSC, true>(h.lv[i], bx, by, pair, S);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's u stores acknowledged
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(h.done + i * h.batch + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The blocks k_search8<LPP, false> listed: persistent workgroups over the list
@@ -1383,21 +896,18 @@ k_search8_head(HeadArgs h)
 // Capped at the tile kernel's 128 VGPRs (spilling on this rare path): with more,
 // its workgroups cannot take the slots another stream's search kernel frees,
 // and the (usually empty) launch waited 70-150 us for that kernel to drain.
-// LPPS: the lane layout that searches the listed blocks (the same 8x8-patch
-// blocks at LPP 2 and 8; LPP 8 needs no spill: 66 VGPRs)
-template <int LPP, bool kPaper = false, bool kFma = false, bool kPhys = false, int LPPS = LPP>
-__global__ void __launch_bounds__(kThreads<LPPS>) __attribute__((amdgpu_waves_per_eu(kWaves<LPPS, LPPS != LPP>)))
+template <int LPP, bool kPaper = false, bool kFma = false, bool kPhys = false>
+__global__ void __launch_bounds__(kThreads<LPP>) __attribute__((amdgpu_waves_per_eu(kWaves<LPP, false>)))
 __attribute__((amdgpu_num_vgpr(128)))
 k_search8_fb(Search8Args a)
 {
-    static_assert(kBX<LPPS> == kBX<LPP>, "listed blocks must be blocks of the searching layout");
-    __shared__ BlockLds<LPPS> S;
+    __shared__ BlockLds<LPP> S;
     const int n = *a.fb_count;
     const int nbx = (a.npw + kBX<LPP> - 1) / kBX<LPP>, nby = (a.nph + kBY - 1) / kBY;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int e = a.fb_list[i];
         const int bx = e % nbx, t = e / nbx;
-        search_block<LPPS, true, kPaper, kFma, kPhys>(a, bx, t % nby, t / nby, S);
+        search_block<LPP, true, kPaper, kFma, kPhys>(a, bx, t % nby, t / nby, S);
         __syncthreads();  // LDS reuse by the next listed block
     }
 }
@@ -1465,9 +975,6 @@ bool search8_lpp1_fits(int steps)
     return (15 * steps + 11) * (7 * steps + 10) <= kTileH * kTSMax<1>;
 }
 
-#ifndef DIS_STATIC_TS
-#define DIS_STATIC_TS 1
-#endif
 // k_search8 with the tile stride the host picked (search8_tile_stride) as a
 // template constant: 65, 66, 68 or 72 (every stride tile_layout picks); others
 // at run time
@@ -1475,7 +982,7 @@ template <int LPP, bool kFallback, bool kPaper, bool kFma>
 static void launch_ts(const Search8Args& a, dim3 grid, hipStream_t s, Timing t)
 {
     const dim3 block(kThreads<LPP>);
-    switch (DIS_STATIC_TS ? a.tile_stride : 0) {
+    switch (a.tile_stride) {
         case 65: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 65>), grid, block, 0, s, a); break;
         case 66: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 66>), grid, block, 0, s, a); break;
         case 68: DIS_LAUNCH(t, (k_search8<LPP, kFallback, kPaper, kFma, false, 68>), grid, block, 0, s, a); break;
@@ -1491,32 +998,17 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     if (L == 1) {
         if (split) {
             DIS_LAUNCH(t, (k_search8<1, false, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
-            if (!DIS_EXP_NO_FB) hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<1, kPaper, kFma>), fb_grid, dim3(kThreads<1>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<1, true, kPaper, kFma>), grid, dim3(kThreads<1>), 0, s, a);
         }
     } else if (L == 2) {
-        if (DIS_FB_MERGED && split && a.fb_decided) {  // the fallback workers appended to the launch (1-D grid)
-            Search8Args m = a;
-            m.fb_wgs = std::min<int>(DIS_FB_MERGED_WGS, (int)fb_grid.x);
-            const dim3 g1((unsigned)((long long)grid.x * grid.y * grid.z + m.fb_wgs));
-            if constexpr (!kPaper)
-                launch_ts<2, false, kPaper, kFma>(m, g1, s, t);
-            else
-                DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), g1, dim3(kThreads<2>), 0, s, m);
-        } else if (split) {
+        if (split) {
             if constexpr (!kPaper)
                 launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             else
                 DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
-            // (DIS_FB_LPP8, exact modes: the listed blocks searched at 8 lanes
-            // per patch, same bits; tolerance mode at 2, whose contracted sums it
-            // shares)
-            if constexpr (DIS_EXP_NO_FB) {
-            } else if constexpr (DIS_FB_LPP8 && !kFma)
-                hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma, false, 8>), fb_grid, dim3(kThreads<8>), 0, s, a);
-            else
-                hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
         }
@@ -1537,10 +1029,7 @@ static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 gr
     if (L == 2) {
         if (split) {
             hipLaunchKernelGGL((k_search8<2, false, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
-            if (DIS_FB_LPP8)
-                hipLaunchKernelGGL((k_search8_fb<2, false, false, true, 8>), fb_grid, dim3(kThreads<8>), 0, s, a);
-            else
-                hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
+            hipLaunchKernelGGL((k_search8_fb<2, false, false, true>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             hipLaunchKernelGGL((k_search8<2, true, false, false, true>), grid, dim3(kThreads<2>), 0, s, a);
         }
@@ -1549,42 +1038,10 @@ static void launch_search8_phys(const Search8Args& a, int L, bool split, dim3 gr
     }
 }
 
-hipError_t launch_search8_head(const HeadArgs& h, hipStream_t s, Timing t)
-{
-    if (h.nlev < 1 || h.nlev > kHeadMax || !h.done || h.batch < 1) return hipErrorInvalidValue;
-    for (int i = 0; i < h.nlev; ++i) {
-        const Search8Args& a = h.lv[i];
-        if (a.lanes_per_patch != 8 || a.paper || a.gdx_plane || a.dense_coarse || a.u_init ||
-            a.tile_stride != h.lv[0].tile_stride || a.tile_stride < kTileW<2> + 1 || a.tile_stride > kTSMax<2> ||
-            (7 * a.steps + 11) * (7 * a.steps + 10) > kTileH * kTSMax<2> ||
-            h.nbx[i] != (a.npw + kBX<8> - 1) / kBX<8> || h.nby[i] != (a.nph + kBY - 1) / kBY ||
-            h.start[i + 1] - h.start[i] != h.nbx[i] * h.nby[i] * h.batch || (i > 0 && !a.u_coarse))
-            return hipErrorInvalidValue;
-    }
-    if (h.start[0] != 0) return hipErrorInvalidValue;
-    const dim3 grid(h.start[h.nlev]), block(kThreads<8>);
-#define DIS_HEAD_LAUNCH(FMA, TS) DIS_LAUNCH(t, (k_search8_head<FMA, TS>), grid, block, 0, s, h)
-    const bool fma = h.lv[0].fma != 0;
-    switch (DIS_STATIC_TS ? h.lv[0].tile_stride : 0) {
-        case 65: if (fma) DIS_HEAD_LAUNCH(true, 65); else DIS_HEAD_LAUNCH(false, 65); break;
-        case 66: if (fma) DIS_HEAD_LAUNCH(true, 66); else DIS_HEAD_LAUNCH(false, 66); break;
-        case 68: if (fma) DIS_HEAD_LAUNCH(true, 68); else DIS_HEAD_LAUNCH(false, 68); break;
-        case 72: if (fma) DIS_HEAD_LAUNCH(true, 72); else DIS_HEAD_LAUNCH(false, 72); break;
-        default: if (fma) DIS_HEAD_LAUNCH(true, 0); else DIS_HEAD_LAUNCH(false, 0); break;
-    }
-#undef DIS_HEAD_LAUNCH
-    return hipGetLastError();
-}
-
 hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing t)
 {
     const int L = a.lanes_per_patch;
-    if (L == 64) {  // one wave per patch: exact, non-paper, virtual padding only
-        if (a.paper || a.fma || a.gdx_plane) return hipErrorInvalidValue;
-        dim3 grid((unsigned)((a.npw * a.nph + 3) / 4), batch);
-        DIS_LAUNCH(t, k_search_wave, grid, dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
+    if (L == 64) return launch_search_wave(a, batch, s, t);  // one wave per patch (dis_search_wave.hip)
     if (L != 1 && L != 2 && L != 4 && L != 8) return hipErrorInvalidValue;
     const int w = L == 1 ? kTileW<1> : kTileW<2>, smax = L == 1 ? kTSMax<1> : kTSMax<2>;
     if (a.tile_stride < w + 1 || a.tile_stride > smax) return hipErrorInvalidValue;
@@ -1596,10 +1053,9 @@ hipError_t launch_search8(const Search8Args& a, int batch, hipStream_t s, Timing
     // k_search8_fb launch over the blocks it listed. (Searching those blocks
     // in place through a non-inlined call instead made every wave of the tile
     // kernel carry a scratch frame: finest launch 940 -> 1346 us; r03.)
-    const bool split = DIS_SPLIT_FB && (L == 1 || L == 2) && a.fb_count && a.fb_list;
-    if (a.fb_decided && (!DIS_FB_MERGED || L != 2 || !split || a.gdx_plane)) return hipErrorInvalidValue;
+    const bool split = (L == 1 || L == 2) && a.fb_count && a.fb_list;
     // persistent fallback workgroups (grid-stride over the list), one per CU
-    const dim3 fb_grid(std::min<long long>(DIS_FB_WGS, (long long)grid.x * grid.y * grid.z));
+    const dim3 fb_grid(std::min<long long>(kFbWgs, (long long)grid.x * grid.y * grid.z));
     if (a.gdx_plane) {  // physical planes (compat): exact, non-paper, LPP 2 or 8
         if ((L != 2 && L != 8) || a.paper || a.fma || !a.gdy_plane || a.pad < 0) return hipErrorInvalidValue;
         launch_search8_phys(a, L, split, grid, fb_grid, s);

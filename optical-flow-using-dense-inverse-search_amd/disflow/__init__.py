@@ -172,8 +172,7 @@ def lib() -> ctypes.CDLL:
 
 
 def build_kind() -> str:
-    """"product", or "experiment" for a knock-out measurement build (wrong values
-    by design, csrc/dis_experiments.h)."""
+    """"product" (the sources carry no compile-time variants since ABI v7)."""
     return lib().dis_build_kind().decode()
 
 
@@ -288,12 +287,11 @@ class DenseInverseSearch:
                                        MEM_DEVICE, stream or None))
 
     def set_variant(self, variant: int) -> None:
-        """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels,
-        fused coarse head), 1 = generic only, 2 / 3 / 4 / 5 = 4 / 2 / 8 / 1 lanes per
-        patch, 6 = one wave per patch, 7 = auto with one launch per coarse level (the
-        default's form), 8 = auto with the coarse levels fused into one launch, 9 = 2
-        lanes per patch with the usable LDS tile capped at 24 pixels (test hook: most
-        blocks take the fallback list and k_search8_fb)."""
+        """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels),
+        1 = generic only, 2 / 3 / 4 / 5 = 4 / 2 / 8 / 1 lanes per patch, 6 = one wave
+        per patch, 9 = 2 lanes per patch with the usable LDS tile capped at 24 pixels
+        (test hook: most blocks take the fallback list and k_search8_fb); 7 and 8
+        were removed in ABI v7."""
         _check(lib().dis_set_kernel_variant(self._ctx, variant))
 
     def set_concurrency(self, streams: int) -> None:

@@ -476,26 +476,26 @@ def test_lanes_per_patch_variants_bitexact(disflow_mod, oracle, preset):
     exp = oracle.calc_from_params(I0, I1, p)
     exp_fb = oracle.calc_from_params(J0, J1, p)
     eng = disflow_mod.DenseInverseSearch(p, W, H)
-    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64"),
-                          (7, "auto, one launch per level"), (8, "auto, fused head")):
+    for variant, name in ((0, "auto"), (3, "LPP2"), (2, "LPP4"), (4, "LPP8"), (5, "LPP1"), (6, "LPP64")):
         eng.set_variant(variant)
         _assert_bitexact(eng.calc(I0, I1), exp, f"{name} vs oracle")
         _assert_bitexact(eng.calc(J0, J1), exp_fb, f"{name} fallback vs oracle")
 
 
-HEAD_CASES = [
-    # (W, H, preset, batch, streams, variant, fma): the fused coarse head
-    # (k_search8_head) against the per-level launches (variant 7) and the oracle
-    (1920, 1080, "MEDIUM", 3, 1, 8, 0),   # levels 6..4 in one launch (3 pairs)
-    (1920, 1080, "MEDIUM", 4, 2, 8, 1),   # two sub-batches, tolerance mode (vs variant 7 only)
-    (640, 480, "ULTRAFAST", 5, 2, 8, 0),  # C 4 .. (levels at 8 lanes per patch)
-    (320, 240, "MEDIUM", 2, 1, 8, 0),     # every level at 8 lanes: the head reaches the finest level
-    (203, 151, "SLOW", 3, 3, 8, 0),       # ragged, F = 0, three sub-batches of one pair
+SUBBATCH_CASES = [
+    # (W, H, preset, batch, streams, fma): batches split into sub-batch streams
+    # against single-pair oracle runs (and, in the tolerance mode, against one
+    # stream: the split must not change a bit either way)
+    (1920, 1080, "MEDIUM", 3, 1, 0),
+    (1920, 1080, "MEDIUM", 4, 2, 1),
+    (640, 480, "ULTRAFAST", 5, 2, 0),
+    (320, 240, "MEDIUM", 2, 1, 0),     # every level at 8 lanes per patch
+    (203, 151, "SLOW", 3, 3, 0),       # ragged, F = 0, three sub-batches of one pair
 ]
 
 
-@pytest.mark.parametrize("W,H,preset,B,streams,variant,fma", HEAD_CASES)
-def test_fused_head_bitexact(disflow_mod, oracle, W, H, preset, B, streams, variant, fma):
+@pytest.mark.parametrize("W,H,preset,B,streams,fma", SUBBATCH_CASES)
+def test_subbatch_streams_bitexact(disflow_mod, oracle, W, H, preset, B, streams, fma):
     p = disflow_mod.preset_params(disflow_mod.Preset[preset], W, H)
     if preset == "SLOW":
         p.iterations = 16
@@ -505,15 +505,39 @@ def test_fused_head_bitexact(disflow_mod, oracle, W, H, preset, B, streams, vari
     eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=B)
     eng.set_concurrency(streams)
     eng.set_precision(fma)
-    eng.set_variant(variant)
     got = eng.calc_batch(I0, I1)
-    eng.set_variant(7 if variant == 8 else 3)  # per-level launches (variant 3: 2 lanes everywhere)
-    ref = eng.calc_batch(I0, I1)
-    if variant == 8:
-        _assert_bitexact(got, ref, "fused head vs per-level launches")
+    eng.set_concurrency(1)
+    _assert_bitexact(got, eng.calc_batch(I0, I1), f"{streams} sub-batch streams vs one")
     if not fma:
         for k in range(B):
             _assert_bitexact(got[k], oracle.calc_from_params(I0[k], I1[k], p), f"pair {k} vs oracle")
+
+
+def test_fallback_counter_follows_graph_replays(disflow_mod):
+    # DIS_STAGE_FALLBACK sums the fallback lists of the sub-batches the last
+    # call ran; a replayed graph runs the sub-batches it was captured with
+    # (a replay of an n = 2 graph after an n = 1 capture used to
+    # report one sub-batch's count)
+    W, H = 320, 256
+    p = disflow_mod.preset_params(disflow_mod.Preset.MEDIUM, W, H)
+    p.iterations = 4
+    pairs = [disflow_mod.synth_pair(60 + k, W, H) for k in range(2)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    levels = range(p.finest_scale, p.coarsest_scale + 1)
+    eng = disflow_mod.DenseInverseSearch(p, W, H, max_batch=2)
+    eng.set_concurrency(2)
+    eng.set_variant(9)  # most blocks through the fallback lists
+    eng.set_graphs(False)
+    ref = {}
+    for n in (2, 1):
+        eng.calc_batch(I0[:n], I1[:n])
+        ref[n] = [eng.fallback_blocks(l) for l in levels]
+    assert sum(ref[2]) > sum(ref[1]) > 0, ref
+    eng.set_graphs(True)
+    for n in (2, 1, 2, 1, 2):
+        eng.calc_batch(I0[:n], I1[:n])
+        assert [eng.fallback_blocks(l) for l in levels] == ref[n], (n, ref)
 
 
 @pytest.mark.gpu

@@ -1,0 +1,78 @@
+"""No compile-time variant can hide in the product sources (VERDICT r04 next
+#5): every kernel alternative that stays must be reachable at run time
+(dis_set_kernel_variant, dis_set_precision, ...) and so exercised by the -m gpu
+tests. Measured-and-rejected variants live as A/B records in DESIGN.md 7, not
+as #if blocks that no build compiles. CPU only: greps of the sources."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "optical-flow-using-dense-inverse-search_amd")
+PRODUCT_DIRS = [os.path.join(PKG, "csrc"), os.path.join(PKG, "cli"), os.path.join(ROOT, "include"),
+                os.path.join(ROOT, "include", "dis")]
+COND = re.compile(r"^\s*#\s*(if|ifdef|ifndef|elif)\b(.*)$")
+# include guards of the public headers: not switches
+GUARDS = {"DIS_ABI_H", "DIS_ORACLE_H"}
+
+
+def _sources(dirs, exts=(".hip", ".h", ".hpp", ".cpp", ".c")):
+    for d in dirs:
+        for f in sorted(os.listdir(d)):
+            if f.endswith(exts):
+                yield os.path.join(d, f)
+
+
+def _conditionals(path):
+    out = []
+    for n, line in enumerate(open(path, encoding="utf-8"), 1):
+        m = COND.match(line)
+        if m:
+            out.append((n, m.group(2)))
+    return out
+
+
+def test_product_sources_have_no_dis_switches():
+    bad = []
+    for p in _sources(PRODUCT_DIRS):
+        for n, expr in _conditionals(p):
+            names = set(re.findall(r"\bDIS_\w+", expr)) - GUARDS
+            if names:
+                bad.append(f"{os.path.relpath(p, ROOT)}:{n}: {sorted(names)}")
+    assert not bad, "compile-time DIS_* switches in product sources (no test builds them):\n" + "\n".join(bad)
+
+
+def test_kernel_files_have_few_conditionals():
+    # at most 15 preprocessor conditionals per kernel file (include guards,
+    # __cplusplus and similar are all that should remain)
+    for p in _sources([os.path.join(PKG, "csrc")], (".hip",)):
+        n = len(_conditionals(p))
+        assert n <= 15, f"{os.path.relpath(p, ROOT)}: {n} preprocessor conditionals"
+
+
+def test_search_kernel_file_size():
+    n = sum(1 for _ in open(os.path.join(PKG, "csrc", "dis_search8.hip")))
+    assert n <= 1250, f"dis_search8.hip has {n} lines"
+
+
+def test_makefile_defines_no_dis_switch():
+    mk = open(os.path.join(PKG, "Makefile")).read()
+    assert not re.search(r"-D\s*DIS_", mk)
+    gd = open(os.path.join(ROOT, "__graft_entry__.py")).read()
+    assert not re.search(r"-D\s*DIS_", gd)
+
+
+def test_oracle_switches_are_all_built():
+    # the oracle (test infrastructure) keeps its rounding-order variants for
+    # the tolerance calibration: each switch must be built by oracle/Makefile's
+    # `variants` target, which __graft_entry__.build() runs and
+    # tests/test_oracle.py's tolerance test loads
+    src = os.path.join(ROOT, "oracle", "dis_oracle.c")
+    used = set()
+    for _, expr in _conditionals(src):
+        used |= set(re.findall(r"\bDIS_\w+", expr))
+    used -= GUARDS
+    mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
+    built = set(re.findall(r"-D(DIS_\w+)", mk))
+    assert used, "the grep is broken"
+    assert used <= built, f"oracle switches never built: {sorted(used - built)}"
+    assert "variants" in open(os.path.join(ROOT, "__graft_entry__.py")).read()

@@ -4,6 +4,10 @@
 resident in HBM, batch per call as given, `steps` timed calls after warmup.
 
   config 1  640x480    ULTRAFAST
+  1cpu      config 1's reference CPU path (BASELINE config 1): the C restatement
+            (oracle/dis_oracle.c at -O3, one pair at a time per process, like
+            src/main.cpp:102-206) on one core and on the job's 16-CPU share --
+            run first, before the GPU is initialised (forked workers)
   config 2  1920x1080  MEDIUM            (as bench.py)
   config 3  3840x2160  MEDIUM
   config 5  3840x2160  SLOW + variational refinement (3 fixed-point iterations per level)
@@ -165,13 +169,36 @@ def run_compat(steps, warmup):
                     "full-resolution flow D2H)"}
 
 
+def run_cpu1(budget_s):
+    """BASELINE config 1 on the host: 640x480 ULTRAFAST through the C
+    restatement, single-core latency and 16-process throughput (bench.py's
+    cpu_baseline on this workload)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    W, H = 640, 480
+    p = disflow.preset_params(disflow.Preset.ULTRAFAST, W, H)
+    workers = min(bench.CPU_WORKER_CAP, len(os.sched_getaffinity(0)))
+    r = bench.cpu_baseline(p, W, H, budget_s, workers)
+    return {"config": "config 1 CPU: 640x480 ULTRAFAST, C restatement (" +
+            os.path.basename(bench.oracle_lib_for_baseline()) + ")",
+            "kind": "port", "pairs_per_s": r["value"], "cores": r["cores"], "pairs": r["pairs"],
+            "single_core_pairs_per_s": r["single_core"]["value"], "single_core_pairs": r["single_core"]["pairs"],
+            "cpu_model": bench.cpu_model(), "budget_s": budget_s,
+            "knobs": {"C": p.coarsest_scale, "F": p.finest_scale, "it": p.iterations, "overlap": p.patch_overlap}}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,2,3,5,2p,2f,3f,colour,compat")
+    ap.add_argument("--configs", default="1cpu,1,2,3,5,2p,2f,3f,colour,compat")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=9.0)
     a = ap.parse_args()
-    for c in a.configs.split(","):
+    cfgs = a.configs.split(",")
+    if "1cpu" in cfgs:  # forks its workers: before anything initialises the GPU
+        cfgs.remove("1cpu")
+        print(json.dumps(run_cpu1(a.cpu_seconds)), flush=True)
+    for c in cfgs:
         if c == "colour":
             r = run_colour(a.steps, a.warmup)
         elif c == "compat":
