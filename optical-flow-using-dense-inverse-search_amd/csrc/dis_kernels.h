@@ -66,9 +66,10 @@ struct Search8Args {
     int* fb_count;            // LPP 1/2: blocks too spread for the LDS tile are listed here
     int* fb_list;             //   (count zeroed before the launch) and redone by k_search8_fb;
                               //   nullptr: one kernel with the global-read path inline
-    int paper;                // template-subtracted residual (k_search8<.., kPaper>)
-    const float2* u_init;     // non-null (paper mode): per-patch initial u from k_paper_init, patch-id
-    long long init_stride;    //   order, float2 per pair
+    int paper;                // template-subtracted residual (k_search8<.., kPaper>) and
+                              //   the residual-weighted coarse-to-fine initialisation, which reads the
+    long long c_plane_off;    //   coarser level's planes (offset in the stack) of size c_W x c_H
+    int c_W, c_H;
     int fma;                  // DIS_PRECISION_FMA: contracted warp / dot products, reciprocal solve
     // compat path (dis_flow_from_pyramids): non-null = the caller's physically
     // padded planes (pad pixels on every side, row stride W + 2 pad; plane_off
@@ -78,21 +79,6 @@ struct Search8Args {
     const float* gdy_plane;
     int pad;
 };
-
-// Paper mode's coarse-to-fine initialisation of level l:
-// for every patch, 2 x the weighted densification of level l+1 evaluated only
-// at the patch's sampled pixel floor(ref / 2) (src/patch_grid.cpp:108-119).
-struct PaperInitArgs {
-    const float2* u_coarse;   // level l+1 patch u (pre-offset), pair stride u_stride
-    float2* init;             // level l initial u per patch (pre-offset), pair stride init_stride
-    const float* img0;        // level l+1 planes of pair 0 (pre-offset), pair stride plane_stride
-    const float* img1;
-    long long u_stride, init_stride, plane_stride;
-    int npw, nph, offw, offh, steps;          // level l grid
-    int c_npw, c_nph, c_offw, c_offh, c_W, c_H;  // level l+1 grid and size
-    int hp;                                   // patch_size / 2
-};
-hipError_t launch_paper_init(const PaperInitArgs& a, int batch, hipStream_t s);
 
 struct DensifyArgs {
     const float2* u;       // patch u of the level (pre-offset)

@@ -511,55 +511,6 @@ hipError_t launch_search_generic(const SearchArgs& a, int ps, int batch, hipStre
     return hipGetLastError();
 }
 
-// Paper-mode initialisation (oracle: densify_paper on level l+1, read at
-// (floor(rx/2), floor(ry/2)), times 2). One thread per level-l patch; a wave
-// owns an 8 x 8 block of patches, x fastest, so its bilinear taps fall in a
-// ~12 x 12 pixel region (a few cache lines per load, not one per lane).
-// grid: (ceil(npw / 16), ceil(nph / 16), batch), block 256 = 2 x 2 waves
-__global__ void __launch_bounds__(256) k_paper_init(PaperInitArgs a)
-{
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int gx = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7);
-    const int gy = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
-    const int pair = blockIdx.z;
-    if (gx >= a.npw || gy >= a.nph) return;
-    const int id = gx * a.nph + gy;
-    const int x = (gx * a.steps + a.offw) >> 1, y = (gy * a.steps + a.offh) >> 1;  // level l+1 pixel
-    const int st = a.steps, hp = a.hp;
-    const float rst = __builtin_amdgcn_rcpf((float)st);  // floordiv_r: exact for |a| < 2^20
-    int cx0 = floordiv_r(x - a.c_offw - hp + st, rst), cx1 = floordiv_r(x - a.c_offw + hp, rst);
-    int cy0 = floordiv_r(y - a.c_offh - hp + st, rst), cy1 = floordiv_r(y - a.c_offh + hp, rst);
-    cx0 = max(cx0, 0);
-    cy0 = max(cy0, 0);
-    cx1 = min(cx1, a.c_npw - 1);
-    cy1 = min(cy1, a.c_nph - 1);
-    const float2* u = a.u_coarse + (size_t)pair * a.u_stride;
-    const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
-    const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
-    const float i0v = I0[(size_t)y * a.c_W + x];
-    float fx = 0.0f, fy = 0.0f, w = 0.0f;
-    for (int cx = cx0; cx <= cx1; ++cx)
-        for (int cy = cy0; cy <= cy1; ++cy) {
-            const float2 v = u[cx * a.c_nph + cy];
-            const float d = bilinear_replicate(I1, a.c_W, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
-            const float c = recip_max1(d);  // 1 / max(1, |d|), correctly rounded (dis_device.h)
-            fx = fx + c * v.x;
-            fy = fy + c * v.y;
-            w = w + c;
-        }
-    if (w > 0) {
-        fx = fx / w;
-        fy = fy / w;
-    }
-    a.init[(size_t)pair * a.init_stride + id] = make_float2(fx * 2, fy * 2);
-}
-
-hipError_t launch_paper_init(const PaperInitArgs& a, int batch, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_paper_init, dim3((a.npw + 15) / 16, (a.nph + 15) / 16, batch), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_densify(const DensifyArgs& a, int batch, hipStream_t s)
 {
     if (a.ps > 16 || a.steps < 1) return hipErrorInvalidValue;  // the staged patch block (kDenPX x kDenPY)

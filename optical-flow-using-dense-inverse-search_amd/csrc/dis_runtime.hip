@@ -528,32 +528,10 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
         a.paper = paper ? 1 : 0;
         if (fast) {
             dis::Search8Args b = make_s8(l);
-            if (paper && !vr && l < g.C) {
-                // weighted initialisation per patch, into this level's (unused) dense slot
-                const dis::LevelGeom& Lc = g.lv[l + 1];
-                dis::PaperInitArgs pi{};
-                pi.u_coarse = pu + Lc.u_off;
-                pi.init = dense + L.dense_off;
-                pi.img0 = img0 + Lc.plane_off;
-                pi.img1 = img1 + Lc.plane_off;
-                pi.u_stride = g.u_stride;
-                pi.init_stride = g.dense_stride;
-                pi.plane_stride = g.plane_stride;
-                pi.npw = L.npw;
-                pi.nph = L.nph;
-                pi.offw = L.offw;
-                pi.offh = L.offh;
-                pi.steps = L.steps;
-                pi.c_npw = Lc.npw;
-                pi.c_nph = Lc.nph;
-                pi.c_offw = Lc.offw;
-                pi.c_offh = Lc.offh;
-                pi.c_W = Lc.W;
-                pi.c_H = Lc.H;
-                pi.hp = g.ps / 2;
-                DIS_HIP(dis::launch_paper_init(pi, n, s));
-                b.u_init = pi.init;
-                b.init_stride = pi.init_stride;
+            if (paper && l < g.C) {  // the weighted coarse-to-fine init reads the coarser level's planes
+                b.c_plane_off = g.lv[l + 1].plane_off;
+                b.c_W = g.lv[l + 1].W;
+                b.c_H = g.lv[l + 1].H;
             }
             if (vr && l < g.C) {  // refined dense flows: init from the coarser level's dense field
                 b.dense_coarse = dense + g.lv[l + 1].dense_off;

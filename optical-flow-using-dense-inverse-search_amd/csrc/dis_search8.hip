@@ -518,10 +518,7 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     const int hp = 4;
     int ga = 0, ha = 0, PH = 0, PN = 0;
     float2 cuv[kCuPer<LPP>];
-    const float2* uc =
-        (a.u_coarse && !a.dense_coarse && !a.u_init) ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
-    const float2 uinit = (a.u_init && active) ? a.u_init[(size_t)pair * a.init_stride + gx * a.nph + gy]
-                                              : make_float2(0.0f, 0.0f);
+    const float2* uc = (a.u_coarse && !a.dense_coarse) ? a.u_coarse + (size_t)pair * a.u_stride : nullptr;
     if (uc) {
         const int xlo = (bgx0 * st + a.offw) >> 1, xhi = (bgx1 * st + a.offw) >> 1;
         const int ylo = (bgy0 * st + a.offh) >> 1, yhi = (bgy1 * st + a.offh) >> 1;
@@ -591,6 +588,39 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
         bnd[3] = -0x7fffffff;
     }
     __syncthreads();
+
+    // paper mode (oracle patch_init_paper): the coarse-to-fine
+    // initialisation is the coarser level's residual-weighted densification
+    // evaluated at the patch's sampled pixel (x, y) = floor(ref / 2): votes of
+    // the covering coarse patches (staged above, patch-id order) weighted by
+    // 1 / max(1, |I1_{l+1}(x + v) - I0_{l+1}(x)|), I1 bilinear with the
+    // replicate border. Before the gradients: fewer registers live.
+    float ix = 0.0f, iy = 0.0f;
+    if constexpr (kPaper) {
+        if (uc && active) {
+            const int x = irx >> 1, y = iry >> 1, cW = a.c_W;
+            const float* I0c = a.img0 + (size_t)pair * a.plane_stride + a.c_plane_off;
+            const float* I1c = a.img1 + (size_t)pair * a.plane_stride + a.c_plane_off;
+            const float i0v = I0c[(size_t)y * cW + x];
+            const int2 xr = crng[gx - bgx0], yr = crng[BX + gy - bgy0];
+            float fx = 0.0f, fy = 0.0f, wt = 0.0f;
+            for (int cx = xr.x; cx <= xr.y; ++cx)
+                for (int cy = yr.x; cy <= yr.y; ++cy) {
+                    const float2 v = cu[cx * PH + cy];
+                    const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
+                    const float c = recip_max1(d);  // correctly rounded (dis_device.h)
+                    fx = fx + c * v.x;
+                    fy = fy + c * v.y;
+                    wt = wt + c;
+                }
+            if (wt > 0) {
+                fx = fx / wt;
+                fy = fy / wt;
+            }
+            ix = fx * 2;
+            iy = fy * 2;
+        }
+    }
 
     // --- 2. template gradients: Sobel (ksize 3, 1/8, reflect-101) of the level
     // image at pixels (rx-4+c, ry-4+j), zero outside the image (zero-padded
@@ -673,11 +703,8 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
     // --- 3. initialisation from the coarser level (src/patch_grid.cpp:108-119):
     // dense_{l+1}(floor(ref/2)) = mean over covering coarse patches (patch-id
     // order, f from +0, weights 0.5: src/patch_grid.cpp:121-182), times 2,
-    // gathered from the staged coarse displacements.
-    float ix = 0.0f, iy = 0.0f;
-    if (a.u_init && active) {  // paper mode: the weighted initialisation (k_paper_init), loaded in step 1
-        ix = uinit.x;
-        iy = uinit.y;
+    // gathered from the staged coarse displacements (paper mode: above).
+    if (kPaper && uc) {
     } else if (a.dense_coarse && active) {
         // from the coarser level's dense flow (refined): src/patch_grid.cpp:108-119
         const float2 d = a.dense_coarse[(size_t)pair * a.dense_stride + (size_t)(iry >> 1) * (W / 2) + (irx >> 1)];
@@ -1004,10 +1031,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
         }
     } else if (L == 2) {
         if (split) {
-            if constexpr (!kPaper)
-                launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
-            else
-                DIS_LAUNCH(t, (k_search8<2, false, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
+            launch_ts<2, false, kPaper, kFma>(a, grid, s, t);
             hipLaunchKernelGGL((k_search8_fb<2, kPaper, kFma>), fb_grid, dim3(kThreads<2>), 0, s, a);
         } else {
             DIS_LAUNCH(t, (k_search8<2, true, kPaper, kFma>), grid, dim3(kThreads<2>), 0, s, a);
@@ -1015,10 +1039,7 @@ static void launch_search8_t(const Search8Args& a, int L, bool split, dim3 grid,
     } else if (L == 4) {
         DIS_LAUNCH(t, (k_search8<4, true, kPaper, kFma>), grid, dim3(kThreads<4>), 0, s, a);
     } else {
-        if constexpr (!kPaper)
-            launch_ts<8, true, kPaper, kFma>(a, grid, s, t);
-        else
-            DIS_LAUNCH(t, (k_search8<8, true, kPaper, kFma>), grid, dim3(kThreads<8>), 0, s, a);
+        launch_ts<8, true, kPaper, kFma>(a, grid, s, t);
     }
 }
 

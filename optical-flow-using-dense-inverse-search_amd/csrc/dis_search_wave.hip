@@ -81,11 +81,7 @@ __global__ void __launch_bounds__(256) k_search_wave(Search8Args a)
 
     // initialisation from the coarser level (src/patch_grid.cpp:108-119)
     float ix = 0.0f, iy = 0.0f;
-    if (a.u_init) {
-        const float2 v = a.u_init[(size_t)pair * a.init_stride + p];
-        ix = v.x;
-        iy = v.y;
-    } else if (a.dense_coarse) {
+    if (a.dense_coarse) {
         const float2 d = a.dense_coarse[(size_t)pair * a.dense_stride + (size_t)(iry >> 1) * (W / 2) + (irx >> 1)];
         ix = d.x * 2;
         iy = d.y * 2;
