@@ -401,6 +401,11 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 }
 
 
+// paper mode: I1 of level F over every tap the window's weighted votes can
+// reach (floats; F == 0 has the twice wider window), staged when it fits
+template <bool UPS>
+constexpr int kPaperStage = UPS ? 56 * 56 : 80 * 80;
+
 // one float4 (two output pixels) of the flow. (Streaming, non-temporal
 // stores made the one-stream kernel trace faster -- the next call's pyramid
 // no longer evicted -- but the two-sub-batch step 2-3 % slower: DESIGN.md 3.)
@@ -469,10 +474,16 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     __shared__ float rtab[K * K + 1];                  // RN(1 / (0.5 n)), n covering patches
     __shared__ float2 dense[kOutSW * kOutSH];
     __shared__ int2 cr[kOutSW], rr[kOutSH];
+    __shared__ float s1[kPaper ? kPaperStage<UPSAMPLE> : 1];  // paper mode: staged I1 (see below)
+    __shared__ int pbox[4];
     const int tid = threadIdx.x;
     const int ox = blockIdx.x * kOutTW, oy = blockIdx.y * kOutTH;
     const int pair = blockIdx.z;
     const float2* u = a.u + (size_t)pair * a.u_stride;
+    if (kPaper && tid == 0) {
+        pbox[0] = pbox[1] = 0x7fffffff;
+        pbox[2] = pbox[3] = -0x7fffffff;
+    }
 
     // level-F window of this tile
     int i0, i1, j0, j1;
@@ -497,6 +508,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const int ga = max(0, floordiv_r(i0 - a.offw - hp + st, rst)), gb = min(a.npw - 1, floordiv_r(i1 - a.offw + hp, rst));
     const int ha = max(0, floordiv_r(j0 - a.offh - hp + st, rst)), hb = min(a.nph - 1, floordiv_r(j1 - a.offh + hp, rst));
     const int PW = gb - ga + 1, PH = hb - ha + 1;  // <= kOutPX x kOutPY (output_fits)
+    float umin_x = INFINITY, umin_y = INFINITY, umax_x = -INFINITY, umax_y = -INFINITY;  // paper mode
     {
         constexpr int NL = (kOutPX * kOutPY + 255) / 256;
         float2 v[NL];
@@ -504,7 +516,14 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         for (int j = 0; j < NL; ++j) {
             const int k = tid + 256 * j;
             const int cx = k / kOutPY, cy = k % kOutPY;
-            v[j] = (cx < PW && cy < PH) ? u[(ga + cx) * a.nph + ha + cy] : make_float2(0.f, 0.f);
+            const bool in = cx < PW && cy < PH;
+            v[j] = in ? u[(ga + cx) * a.nph + ha + cy] : make_float2(0.f, 0.f);
+            if (kPaper && in) {
+                umin_x = fminf(umin_x, v[j].x);
+                umax_x = fmaxf(umax_x, v[j].x);
+                umin_y = fminf(umin_y, v[j].y);
+                umax_y = fmaxf(umax_y, v[j].y);
+            }
         }
         // new_u = u * 0.5 (src/patch_grid.cpp:156), formed once per patch (paper mode: u itself)
 #pragma unroll
@@ -528,6 +547,50 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                                   min(floordiv_r(py - a.offh + hp, rst), hb) - ha);
     }
     __syncthreads();
+    // paper mode: every vote samples I1 (bilinear, replicate border) at
+    // X = clamp(RN(x + u.x), -1, W) for a window pixel x and a staged patch's
+    // u, so its taps floor(X), floor(X) + 1 lie in [max(i0 + floor(min u.x),
+    // -1), min(i1 + floor(max u.x) + 1, W) + 1] (likewise in y). Staged in LDS
+    // by logical position, each entry the replicate-clamped pixel the global
+    // read would return, when that box fits; else the votes read I1 globally.
+    int bx0 = 0, by0 = 0, sws = 0;
+    bool staged = false;
+    if constexpr (kPaper) {
+        auto fl = [](float v) { return (int)fminf(fmaxf(floorf(v), -1048576.0f), 1048576.0f); };
+        int m0 = umin_x <= umax_x ? fl(umin_x) : 0x7fffffff, m1 = umin_y <= umax_y ? fl(umin_y) : 0x7fffffff;
+        int m2 = umin_x <= umax_x ? fl(umax_x) : -0x7fffffff, m3 = umin_y <= umax_y ? fl(umax_y) : -0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m0 = min(m0, __shfl_xor(m0, o));
+            m1 = min(m1, __shfl_xor(m1, o));
+            m2 = max(m2, __shfl_xor(m2, o));
+            m3 = max(m3, __shfl_xor(m3, o));
+        }
+        if ((tid & 63) == 0) {
+            atomicMin(&pbox[0], m0);
+            atomicMin(&pbox[1], m1);
+            atomicMax(&pbox[2], m2);
+            atomicMax(&pbox[3], m3);
+        }
+        __syncthreads();
+        if (pbox[0] != 0x7fffffff) {
+            bx0 = max(i0 + pbox[0], -1);
+            by0 = max(j0 + pbox[1], -1);
+            const int bx1 = min(i1 + pbox[2] + 1, a.wF) + 1, by1 = min(j1 + pbox[3] + 1, a.hF) + 1;
+            sws = bx1 - bx0 + 1;
+            const int shs = by1 - by0 + 1;
+            staged = sws > 0 && shs > 0 && sws * shs <= kPaperStage<UPSAMPLE>;
+            if (staged) {
+                const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
+                const float rsw = __builtin_amdgcn_rcpf((float)sws);
+                for (int k = tid; k < sws * shs; k += 256) {
+                    const int r = floordiv_r(k, rsw), c = k - r * sws;
+                    s1[k] = I1[(size_t)clampi(by0 + r, 0, a.hF - 1) * a.wF + clampi(bx0 + c, 0, a.wF - 1)];
+                }
+            }
+        }
+        __syncthreads();
+    }
     const float sc = a.sc;
     const float rrw = __builtin_amdgcn_rcpf((float)rw);  // k / rw by floordiv_r: exact for k < 2^12
     for (int k = tid; k < rw * rh; k += 256) {
@@ -542,14 +605,26 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
             const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
             const float i0v = I0[(size_t)yg * a.wF + xg];
+            const float xf = (float)xg, yf = (float)yg;
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     if ((xr.x + i <= xr.y) && (yr.x + j <= yr.y)) {
                         const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
-                        const float d =
-                            bilinear_replicate(I1, a.wF, a.hF, (float)xg + t.x, (float)yg + t.y) - i0v;
+                        float d;
+                        if (staged) {  // bilinear_replicate's expressions on the staged taps
+                            const float X = fminf(fmaxf(xf + t.x, -1.0f), (float)a.wF);
+                            const float Y = fminf(fmaxf(yf + t.y, -1.0f), (float)a.hF);
+                            const float fx0 = floorf(X), fy0 = floorf(Y);
+                            const float ax = X - fx0, ay = Y - fy0;
+                            const float* q = s1 + ((int)fy0 - by0) * sws + ((int)fx0 - bx0);
+                            const float top = (1.0f - ax) * q[0] + ax * q[1];
+                            const float bot = (1.0f - ax) * q[sws] + ax * q[sws + 1];
+                            d = ((1.0f - ay) * top + ay * bot) - i0v;
+                        } else {
+                            d = bilinear_replicate(I1, a.wF, a.hF, xf + t.x, yf + t.y) - i0v;
+                        }
                         const float cw = recip_max1(d);  // correctly rounded (dis_device.h)
                         fx = fx + cw * t.x;
                         fy = fy + cw * t.y;

@@ -23,6 +23,7 @@
 // floats, in a context workspace of kVarRefPlanes planes per pair.
 #include <hip/hip_runtime.h>
 
+#include "dis_device.h"
 #include "dis_kernels.h"
 
 namespace dis {
@@ -98,31 +99,75 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
     const float* I0 = L.img0 + (size_t)pr * L.plane_stride;
     const float* I1 = L.img1 + (size_t)pr * L.plane_stride;
     const float2* fl = L.flow + (size_t)pr * L.flow_stride;
-    // 1. flow and the warped I1 over the tile +-4
-    for (int k = tid; k < kFW * kFH; k += 256) {
+    // Every load of a phase is issued before any is consumed (unrolled, fixed
+    // trip counts): the flow over the tile +-4, I0x / I0y over the tile +-2 and
+    // the tile's I0 in one round, then the warp's bilinear taps (which need the
+    // flow) in a second -- two memory latencies per workgroup instead of one
+    // per loop iteration.
+    constexpr int NF = (kFW * kFH + 255) / 256, NG = (kGW * kGH + 255) / 256, NP = kLW * kLH / 256;
+    float2 f[NF];
+    float gx0[NG], gy0[NG], i0p[NP];
+#pragma unroll
+    for (int t = 0; t < NF; ++t) {
+        const int k = min(tid + 256 * t, kFW * kFH - 1);
+        const int ly = k / kFW, lx = k - ly * kFW;
+        f[t] = fl[(size_t)clampi_(y0 - 4 + ly, 0, H - 1) * W + clampi_(x0 - 4 + lx, 0, W - 1)];
+    }
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+        const int k = min(tid + 256 * t, kGW * kGH - 1);
+        const int ly = k / kGW, lx = k - ly * kGW;
+        const size_t i = (size_t)clampi_(y0 - 2 + ly, 0, H - 1) * W + clampi_(x0 - 2 + lx, 0, W - 1);
+        gx0[t] = plane(L, pr, P_I0X)[i];
+        gy0[t] = plane(L, pr, P_I0Y)[i];
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+        const int k = tid + 256 * t;
+        const int ly = k / kLW, lx = k - ly * kLW;
+        i0p[t] = I0[(size_t)min(y0 + ly, H - 1) * W + min(x0 + lx, W - 1)];
+    }
+    // 1. the warped I1 over the tile +-4 (I1 at the clamped position + its flow)
+    float ta[NF], tb[NF], tc[NF], td[NF], wfx[NF], wfy[NF];
+#pragma unroll
+    for (int t = 0; t < NF; ++t) {
+        const int k = min(tid + 256 * t, kFW * kFH - 1);
         const int ly = k / kFW, lx = k - ly * kFW;
         const int gx = clampi_(x0 - 4 + lx, 0, W - 1), gy = clampi_(y0 - 4 + ly, 0, H - 1);
-        const float2 f = fl[(size_t)gy * W + gx];
-        sF[ly][lx] = f;
-        float X = (float)gx + f.x, Y = (float)gy + f.y;
+        float X = (float)gx + f[t].x, Y = (float)gy + f[t].y;
         X = fminf(fmaxf(X, -1.0f), (float)W);
         Y = fminf(fmaxf(Y, -1.0f), (float)H);
         const float fx0 = floorf(X), fy0 = floorf(Y);
         const int xa = (int)fx0, ya = (int)fy0;
-        const float fx = X - fx0, fy = Y - fy0;
+        wfx[t] = X - fx0;
+        wfy[t] = Y - fy0;
         const int c0 = clampi_(xa, 0, W - 1), c1 = clampi_(xa + 1, 0, W - 1);
         const float* r0 = I1 + (size_t)clampi_(ya, 0, H - 1) * W;
         const float* r1 = I1 + (size_t)clampi_(ya + 1, 0, H - 1) * W;
-        const float top = (1.0f - fx) * r0[c0] + fx * r0[c1];
-        const float bot = (1.0f - fx) * r1[c0] + fx * r1[c1];
+        ta[t] = r0[c0];
+        tb[t] = r0[c1];
+        tc[t] = r1[c0];
+        td[t] = r1[c1];
+    }
+#pragma unroll
+    for (int t = 0; t < NF; ++t) {
+        const int k = tid + 256 * t;
+        if (k >= kFW * kFH) break;
+        const int ly = k / kFW, lx = k - ly * kFW;
+        const float fx = wfx[t], fy = wfy[t];
+        sF[ly][lx] = f[t];
+        const float top = (1.0f - fx) * ta[t] + fx * tb[t];
+        const float bot = (1.0f - fx) * tc[t] + fx * td[t];
         sI[ly][lx] = (1.0f - fy) * top + fy * bot;
     }
     // 2. I0x, I0y over the tile +-2
-    for (int k = tid; k < kGW * kGH; k += 256) {
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+        const int k = tid + 256 * t;
+        if (k >= kGW * kGH) break;
         const int ly = k / kGW, lx = k - ly * kGW;
-        const size_t i = (size_t)clampi_(y0 - 2 + ly, 0, H - 1) * W + clampi_(x0 - 2 + lx, 0, W - 1);
-        sGx[ly][lx] = plane(L, pr, P_I0X)[i];
-        sGy[ly][lx] = plane(L, pr, P_I0Y)[i];
+        sGx[ly][lx] = gx0[t];
+        sGy[ly][lx] = gy0[t];
     }
     __syncthreads();
     // 3. Wx, Wy over the tile +-2; smoothness weights (forward differences, 0
@@ -153,7 +198,9 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
     __syncthreads();
     // 4. per pixel: the data weights at the current flow and the normal
     //    equations of the linearised energy in (du, dv)
-    for (int k = tid; k < kLW * kLH; k += 256) {
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+        const int k = tid + 256 * t;
         const int ly = k / kLW, lx = k - ly * kLW;
         const int x = x0 + lx, y = y0 + ly;
         if (x >= W || y >= H) continue;
@@ -162,7 +209,7 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
         const float wx = sWx[gy][gx], wy = sWy[gy][gx], i0x = sGx[gy][gx], i0y = sGy[gy][gx];
         const float Ix = 0.5f * (wx + i0x);
         const float Iy = 0.5f * (wy + i0y);
-        const float Iz = sI[fy][fx] - I0[i];
+        const float Iz = sI[fy][fx] - i0p[t];
         const float Ixx = 0.5f * (d5(sWx[gy][gx - 2], sWx[gy][gx - 1], sWx[gy][gx + 1], sWx[gy][gx + 2]) +
                                   d5(sGx[gy][gx - 2], sGx[gy][gx - 1], sGx[gy][gx + 1], sGx[gy][gx + 2]));
         const float Ixy = 0.5f * (d5(sWx[gy - 2][gx], sWx[gy - 1][gx], sWx[gy + 1][gx], sWx[gy + 2][gx]) +
@@ -207,24 +254,30 @@ constexpr int kSRows = kSRH / kSWaves;   // region rows per wave
 static_assert(kSHY >= 2 * kVarRefSor - 1 && kSHX >= 2 * kVarRefSor - 1, "SOR halo: one pixel per half-sweep after the first");
 
 // one pixel's equation: the SOR update reads its 4 neighbours of the other
-// colour; at the image border the neighbour is the pixel itself (weight 0)
+// colour; at the image border the neighbour is the pixel itself (weight 0).
+// r1, r2 = RN(1 / d1), RN(1 / d2): each of the pixel's 5 updates divides by
+// the same d1, d2, so the division is div_pre (correctly rounded from the
+// reciprocal, dis_device.h) instead of the IEEE sequence; numerators below
+// 2^-60 (whose remainders could leave the normal range) take IEEE division
+// (The pixel's own du, dv live only in LDS, read back per update: the
+// reciprocals then fit the 128 VGPRs of 4 waves per SIMD.)
 struct SorPx {
-    float b1, b2, a12, d1, d2, wl, wr, wu, wd, du, dv;
-    unsigned nb;  // bit 0: x > 0, 1: x < W-1, 2: y > 0, 3: y < H-1, 4: in image
+    float b1, b2, a12, d1, d2, r1, r2, s, sl, su;
 };
 
-__global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
+__device__ __forceinline__ float sor_div(float a, float b, float r)
 {
-    // [column parity][region row + 1][pair + 1]; border cells stay 0
-    __shared__ float sU[2][kSRH + 2][kSQ + 2], sV[2][kSRH + 2][kSQ + 2];
-    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
-    const int q = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = blockIdx.x * kSTW, y0 = blockIdx.y * kSTH;
-    const int xs = x0 - kSHX, ys = y0 - kSHY;  // xs even
-    for (int k = tid; k < 2 * (kSRH + 2) * (kSQ + 2); k += 1024) {
-        (&sU[0][0][0])[k] = 0.0f;
-        (&sV[0][0][0])[k] = 0.0f;
-    }
+    if (a != 0.0f && fabsf(a) < 0x1p-60f) return a / b;
+    return div_pre(a, b, r);
+}
+
+// kInt: every pixel of the region and its 4 neighbours inside the image (no
+// border masks; most tiles of a level)
+template <bool kInt>
+__device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][kSQ + 2],
+                                         float (&sV)[2][kSRH + 2][kSQ + 2], int q, int wv, int xs, int ys, int pr)
+{
+    const int W = L.W, H = L.H;
     SorPx P[kSRows][2];
     const float* B1 = plane(L, pr, P_B1);
     const float* B2 = plane(L, pr, P_B2);
@@ -239,12 +292,10 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
         for (int c = 0; c < 2; ++c) {
             SorPx& p = P[j][c];
             const int x = xs + 2 * q + c;
-            const bool in = x >= 0 && x < W && y >= 0 && y < H;
-            p.nb = in ? (16u | (x > 0 ? 1u : 0u) | (x < W - 1 ? 2u : 0u) | (y > 0 ? 4u : 0u) | (y < H - 1 ? 8u : 0u)) : 0u;
+            const bool in = kInt || (x >= 0 && x < W && y >= 0 && y < H);
             p.b1 = p.b2 = p.a12 = 0.0f;
             p.d1 = p.d2 = 1.0f;
-            p.wl = p.wr = p.wu = p.wd = 0.0f;
-            p.du = p.dv = 0.0f;
+            p.s = p.sl = p.su = 0.0f;
             if (in) {
                 const size_t i = (size_t)y * W + x;
                 p.b1 = B1[i];
@@ -252,15 +303,20 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
                 p.a12 = A12[i];
                 p.d1 = D1[i];
                 p.d2 = D2[i];
-                const float s = SW[i];
-                p.wl = x > 0 ? SW[i - 1] : 0.0f;
-                p.wr = x < W - 1 ? s : 0.0f;
-                p.wu = y > 0 ? SW[i - W] : 0.0f;
-                p.wd = y < H - 1 ? s : 0.0f;
+                p.s = SW[i];
+                p.sl = (kInt || x > 0) ? SW[i - 1] : 0.0f;
+                p.su = (kInt || y > 0) ? SW[i - W] : 0.0f;
             }
         }
     }
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSRows; ++j)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            P[j][c].r1 = 1.0f / P[j][c].d1;
+            P[j][c].r2 = 1.0f / P[j][c].d2;
+        }
+    __syncthreads();  // (the caller's zero fill of sU / sV)
     for (int sweep = 0; sweep < kVarRefSor; ++sweep) {
 #pragma unroll
         for (int colour = 0; colour < 2; ++colour) {
@@ -274,20 +330,23 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
                 for (int c = 0; c < 2; ++c) {
                     if (c != cpar) continue;
                     SorPx& p = P[j][c];
-                    if (!(p.nb & 16u)) continue;
+                    const int x = xs + 2 * q + c;
+                    if (!kInt && !(x >= 0 && x < W && y >= 0 && y < H)) continue;
+                    const bool hl = kInt || x > 0, hr = kInt || x < W - 1, hu = kInt || y > 0, hd = kInt || y < H - 1;
+                    const float wl = hl ? p.sl : 0.0f, wr = hr ? p.s : 0.0f;
+                    const float wu = hu ? p.su : 0.0f, wd = hd ? p.s : 0.0f;
+                    const float du = sU[c][r + 1][q + 1], dv = sV[c][r + 1][q + 1];
                     // neighbours (other parity): same row left / right, rows above / below same parity
                     const int o = 1 - c;
                     const int ql = c == 0 ? q : q + 1, qr = c == 0 ? q + 1 : q + 2;
-                    const float ul = (p.nb & 1u) ? sU[o][r + 1][ql] : p.du, ur = (p.nb & 2u) ? sU[o][r + 1][qr] : p.du;
-                    const float uu = (p.nb & 4u) ? sU[c][r][q + 1] : p.du, ud = (p.nb & 8u) ? sU[c][r + 2][q + 1] : p.du;
-                    const float vl = (p.nb & 1u) ? sV[o][r + 1][ql] : p.dv, vr = (p.nb & 2u) ? sV[o][r + 1][qr] : p.dv;
-                    const float vu = (p.nb & 4u) ? sV[c][r][q + 1] : p.dv, vd = (p.nb & 8u) ? sV[c][r + 2][q + 1] : p.dv;
-                    const float sdu = ((p.wl * ul + p.wr * ur) + p.wu * uu) + p.wd * ud;
-                    const float nu = (1.0f - kOmega) * p.du + kOmega * (((p.b1 + sdu) - p.a12 * p.dv) / p.d1);
-                    const float sdv = ((p.wl * vl + p.wr * vr) + p.wu * vu) + p.wd * vd;
-                    const float nv = (1.0f - kOmega) * p.dv + kOmega * (((p.b2 + sdv) - p.a12 * nu) / p.d2);
-                    p.du = nu;
-                    p.dv = nv;
+                    const float ul = hl ? sU[o][r + 1][ql] : du, ur = hr ? sU[o][r + 1][qr] : du;
+                    const float uu = hu ? sU[c][r][q + 1] : du, ud = hd ? sU[c][r + 2][q + 1] : du;
+                    const float vl = hl ? sV[o][r + 1][ql] : dv, vr = hr ? sV[o][r + 1][qr] : dv;
+                    const float vu = hu ? sV[c][r][q + 1] : dv, vd = hd ? sV[c][r + 2][q + 1] : dv;
+                    const float sdu = ((wl * ul + wr * ur) + wu * uu) + wd * ud;
+                    const float nu = (1.0f - kOmega) * du + kOmega * sor_div((p.b1 + sdu) - p.a12 * dv, p.d1, p.r1);
+                    const float sdv = ((wl * vl + wr * vr) + wu * vu) + wd * vd;
+                    const float nv = (1.0f - kOmega) * dv + kOmega * sor_div((p.b2 + sdv) - p.a12 * nu, p.d2, p.r2);
                     sU[c][r + 1][q + 1] = nu;
                     sV[c][r + 1][q + 1] = nv;
                 }
@@ -304,14 +363,31 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
         const int y = ys + r;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const int lx = 2 * q + c - kSHX;
-            const SorPx& p = P[j][c];
-            if (lx < 0 || lx >= kSTW || !(p.nb & 16u)) continue;
-            float2* f = fl + (size_t)y * W + (xs + 2 * q + c);
+            const int lx = 2 * q + c - kSHX, x = xs + 2 * q + c;
+            if (lx < 0 || lx >= kSTW || (!kInt && !(x >= 0 && x < W && y >= 0 && y < H))) continue;
+            float2* f = fl + (size_t)y * W + x;
             const float2 v = *f;
-            *f = make_float2(v.x + p.du, v.y + p.dv);
+            *f = make_float2(v.x + sU[c][r + 1][q + 1], v.y + sV[c][r + 1][q + 1]);
         }
     }
+}
+
+__global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
+{
+    // [column parity][region row + 1][pair + 1]; border cells stay 0
+    __shared__ float sU[2][kSRH + 2][kSQ + 2], sV[2][kSRH + 2][kSQ + 2];
+    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
+    const int q = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = blockIdx.x * kSTW, y0 = blockIdx.y * kSTH;
+    const int xs = x0 - kSHX, ys = y0 - kSHY;  // xs even
+    for (int k = tid; k < 2 * (kSRH + 2) * (kSQ + 2); k += 1024) {
+        (&sU[0][0][0])[k] = 0.0f;
+        (&sV[0][0][0])[k] = 0.0f;
+    }
+    if (xs >= 1 && xs + 2 * kSQ <= W - 1 && ys >= 1 && ys + kSRH <= H - 1)
+        sor_tile<true>(L, sU, sV, q, wv, xs, ys, pr);
+    else
+        sor_tile<false>(L, sU, sV, q, wv, xs, ys, pr);
 }
 
 }  // namespace
