@@ -859,26 +859,34 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             });
         }
     } else if constexpr (kFallback) {
+        // taps read through a buffer descriptor of the (padded) plane: 32-bit
+        // byte offsets from its first pixel, the replicate clamping done on
+        // the indices -- the same values as I1[clamp(row) * ld + clamp(col)]
+        // without 64-bit address arithmetic per tap (fewer VGPRs and VALU)
+        const unsigned long long pb = reinterpret_cast<unsigned long long>(I1 + (ptrdiff_t)lo * ld + lo);
+        const unsigned long long pu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pb >> 32)) << 32) |
+                                      (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pb);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(pu), (short)0, (H + 2 * pad) * ld * (int)sizeof(float), 0x00020000);
+        const int rmax = H - 1 + pad - lo, cmax = W - 1 + pad - lo;
+        auto gtap = [=](int y0, int x0) {
+            return [=](int k, int c) {
+                const int r = clampi(y0 + k - lo, 0, rmax), cc = clampi(x0 + c - lo, 0, cmax);
+                return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (r * ld + cc) * 4, 0, 0));
+            };
+        };
         if constexpr (kSplit) {
             if (valid) {
                 iterate_split<true, kPaper, kFma>(a, lu, gdx, gdy, q, q ? ry : rx, q ? iy : ix, own_y ? bt1 : bt0, &uv,
                                                   [&](int cv) {
                                                       const int cp = xor1i(cv);
-                                                      const int y0 = (q ? cv : cp) - 5, x0 = (q ? cp : cv) - 5 + 4 * q;
-                                                      return [=](int k, int c) {
-                                                          return I1[(ptrdiff_t)clampi(y0 + k, lo, H - 1 + pad) * ld +
-                                                                    clampi(x0 + c, lo, W - 1 + pad)];
-                                                      };
+                                                      return gtap((q ? cv : cp) - 5, (q ? cp : cv) - 5 + 4 * q);
                                                   });
             }
         } else if (valid) {
             const int qb = LPP == 2 ? 4 * q : LPP == 1 ? 0 : q;
-            iterate<LPP, true, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1, [&](const Warp& w) {
-                const int y0 = w.Y - 5, x0 = w.X - 5 + qb;
-                return [=](int k, int c) {
-                    return I1[(ptrdiff_t)clampi(y0 + k, lo, H - 1 + pad) * ld + clampi(x0 + c, lo, W - 1 + pad)];
-                };
-            });
+            iterate<LPP, true, kPaper, kFma>(a, lu, gdx, gdy, rx, ry, ix, iy, bt0, bt1, &u0, &u1,
+                                             [&](const Warp& w) { return gtap(w.Y - 5, w.X - 5 + qb); });
         }
     } else if (any_valid) {
         // too spread for the tile: k_search8_fb redoes this block
