@@ -211,7 +211,10 @@ dis_status dis_debug_dump(dis_ctx* ctx, int stage, int level, int pair, float* d
 /* Per-kernel timing with HIP events recorded on the context's launch stream
  * around every launch of the named kernel class (bench / roofline use).
  * kernel: 0 = fused pyramid, 1 = patch search (all levels), 2 = patch search
- * (finest level only), 3 = fused densify+upsample+crop. Enabling timing while
+ * (finest level only), 3 = fused densify+upsample+crop, 4 / 5 = variational
+ * refinement's linearisation / SOR launches at the finest level (ABI v7;
+ * timing replaces the refinement's per-level graphs by eager launches).
+ * Enabling timing while
  * it is off starts a fresh measurement (accumulated launches and times are
  * cleared); dis_kernel_time returns the totals since then (the event pool
  * grows as needed, so no launch is left out; DIS_ERR_DEVICE if event creation

@@ -40,8 +40,11 @@ __device__ __forceinline__ float bilinear_replicate(const float* __restrict__ I,
     const int xa = (int)fx0, ya = (int)fy0;
     const float fx = X - fx0, fy = Y - fy0;
     const int c0 = clampi(xa, 0, W - 1), c1 = clampi(xa + 1, 0, W - 1);
-    const unsigned o0 = (unsigned)(clampi(ya, 0, H - 1) * W), o1 = (unsigned)(clampi(ya + 1, 0, H - 1) * W);
-    const float top = (1.0f - fx) * I[o0 + c0] + fx * I[o0 + c1];  // 32-bit offsets: a plane < 2^31 floats
+    // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): row < H and
+    // W are < 2^24 and the product < 2^31 (a plane < 2^31 floats)
+    const unsigned o0 = __umul24((unsigned)clampi(ya, 0, H - 1), (unsigned)W);
+    const unsigned o1 = __umul24((unsigned)clampi(ya + 1, 0, H - 1), (unsigned)W);
+    const float top = (1.0f - fx) * I[o0 + c0] + fx * I[o0 + c1];
     const float bot = (1.0f - fx) * I[o1 + c0] + fx * I[o1 + c1];
     return (1.0f - fy) * top + fy * bot;
 }

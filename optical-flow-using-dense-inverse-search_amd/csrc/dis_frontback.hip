@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                             const float Y = fminf(fmaxf(yf + t.y, -1.0f), (float)a.hF);
                             const float fx0 = floorf(X), fy0 = floorf(Y);
                             const float ax = X - fx0, ay = Y - fy0;
-                            const float* q = s1 + ((int)fy0 - by0) * sws + ((int)fx0 - bx0);
+                            const float* q = s1 + __mul24((int)fy0 - by0, sws) + ((int)fx0 - bx0);
                             const float top = (1.0f - ax) * q[0] + ax * q[1];
                             const float bot = (1.0f - ax) * q[sws] + ax * q[sws + 1];
                             d = ((1.0f - ay) * top + ay * bot) - i0v;

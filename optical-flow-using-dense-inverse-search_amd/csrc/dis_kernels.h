@@ -179,6 +179,10 @@ struct VarRefArgs {
     long long ws_plane, ws_stride;
     int W, H, iters;
 };
-hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s);
+// tfn (optional, kernel timing): events for each k_vr_lin (kind 0) and
+// k_vr_sor (kind 1) launch
+typedef Timing (*VarRefTiming)(void* ctx, int kind);
+hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s, VarRefTiming tfn = nullptr,
+                             void* tctx = nullptr);
 
 }  // namespace dis

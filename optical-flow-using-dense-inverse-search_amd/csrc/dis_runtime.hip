@@ -203,8 +203,9 @@ struct dis_ctx {
     std::vector<hipEvent_t> pool;
     std::vector<Rec> recs;
     size_t pool_next = 0;
-    int launches[4] = {0, 0, 0, 0};
-    double total_ms[4] = {0, 0, 0, 0};
+    static constexpr int kKinds = 6;  // dis_kernel_time classes
+    int launches[kKinds] = {};
+    double total_ms[kKinds] = {};
     long long dropped = 0;  // records lost to a failed event creation (dis_kernel_time fails then)
 };
 
@@ -565,6 +566,11 @@ dis_status run_batch(dis_ctx* c, int sub, int n, int p0, const uint8_t* I0, cons
             v.W = L.W;
             v.H = L.H;
             v.iters = c->p.var_refine_iters;
+            if (c->timing) {  // eager, events around the finest level's refinement launches
+                auto tf = [](void* cc, int kind) { return timing(static_cast<dis_ctx*>(cc), 4 + kind); };
+                DIS_HIP(dis::launch_var_refine(v, n, s, l == g.F ? +tf : nullptr, c));
+                continue;
+            }
             auto& G = c->vrg[sub][l];  // the level's launches replayed as one HIP graph
             if (G.n != n || G.p0 != p0) {
                 if (G.exec) hipGraphExecDestroy(G.exec);
@@ -1258,7 +1264,7 @@ dis_status dis_set_kernel_timing(dis_ctx* c, int enable)
         for (auto& r : c->recs) DIS_HIP(hipEventSynchronize(r.b));
         c->recs.clear();
         c->pool_next = 0;
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < dis_ctx::kKinds; ++k) {
             c->launches[k] = 0;
             c->total_ms[k] = 0.0;
         }
@@ -1270,13 +1276,13 @@ dis_status dis_set_kernel_timing(dis_ctx* c, int enable)
 
 dis_status dis_kernel_time(dis_ctx* c, int kernel, int* launches, double* total_ms)
 {
-    if (!c || kernel < 0 || kernel > 3) return fail(DIS_ERR_INVALID_ARGUMENT, "bad argument");
+    if (!c || kernel < 0 || kernel >= dis_ctx::kKinds) return fail(DIS_ERR_INVALID_ARGUMENT, "bad argument");
     DIS_HIP(hipSetDevice(c->device));
     for (auto& r : c->recs) {
         DIS_HIP(hipEventSynchronize(r.b));
         float ms = 0.f;
         DIS_HIP(hipEventElapsedTime(&ms, r.a, r.b));
-        if (r.kind >= 0 && r.kind < 4) {
+        if (r.kind >= 0 && r.kind < dis_ctx::kKinds) {
             c->launches[r.kind] += 1;
             c->total_ms[r.kind] += ms;
         }

@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
 
 }  // namespace
 
-hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s)
+hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s, VarRefTiming tfn, void* tctx)
 {
     if (a.iters <= 0) return hipSuccess;
     Lvl L;
@@ -413,8 +413,10 @@ hipError_t launch_var_refine(const VarRefArgs& a, int n, hipStream_t s)
     const dim3 glin((a.W + kLW - 1) / kLW, (a.H + kLH - 1) / kLH, nn);
     const dim3 gsor((a.W + kSTW - 1) / kSTW, (a.H + kSTH - 1) / kSTH, nn);
     for (int it = 0; it < a.iters; ++it) {
-        hipLaunchKernelGGL(k_vr_lin, glin, dim3(256), 0, s, L);
-        hipLaunchKernelGGL(k_vr_sor, gsor, dim3(1024), 0, s, L);
+        const Timing tl = tfn ? tfn(tctx, 0) : Timing{};
+        DIS_LAUNCH(tl, k_vr_lin, glin, dim3(256), 0, s, L);
+        const Timing ts = tfn ? tfn(tctx, 1) : Timing{};
+        DIS_LAUNCH(ts, k_vr_sor, gsor, dim3(1024), 0, s, L);
     }
     return hipGetLastError();
 }

@@ -48,7 +48,7 @@ STAGE_IMG0, STAGE_IMG1, STAGE_DX0, STAGE_DY0, STAGE_PATCH_U, STAGE_DENSE, STAGE_
 
 PRECISION_EXACT, PRECISION_FMA = 0, 1
 
-KERNEL_PYRAMID, KERNEL_SEARCH, KERNEL_SEARCH_FINEST, KERNEL_DENSIFY = range(4)
+KERNEL_PYRAMID, KERNEL_SEARCH, KERNEL_SEARCH_FINEST, KERNEL_DENSIFY, KERNEL_VR_LIN, KERNEL_VR_SOR = range(6)
 
 # Every symbol include/dis_abi.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (

@@ -69,3 +69,26 @@ def test_config5_full_preset_properties(disflow_mod, oracle):
         assert e_ref < e_plain, (k, e_ref, e_plain)
         epe = np.sqrt(((batch[k] - gt) ** 2).sum(-1))
         assert np.median(epe) < 1.0, np.median(epe)
+
+
+def test_refinement_kernel_timing_eager_path_bitexact(disflow_mod):
+    # dis_kernel_time classes 4 / 5 (ABI v7): under kernel timing the
+    # refinement launches run eagerly with events around the finest level's
+    # k_vr_lin / k_vr_sor instead of replaying the per-level graphs -- the
+    # flow must not change, and the counts follow the fixed-point iterations
+    w, h = 640, 480
+    p = disflow_mod.preset_params(disflow_mod.Preset.SLOW, w, h)
+    p.iterations = 8
+    I0, I1 = disflow_mod.synth_pair(520, w, h)
+    eng = disflow_mod.DenseInverseSearch(p, w, h)
+    ref = eng.calc(I0, I1)
+    eng.set_kernel_timing(True)
+    got = eng.calc(I0, I1)
+    got2 = eng.calc(I0, I1)
+    n_lin, ms_lin = eng.kernel_time(disflow_mod.KERNEL_VR_LIN)
+    n_sor, ms_sor = eng.kernel_time(disflow_mod.KERNEL_VR_SOR)
+    eng.set_kernel_timing(False)
+    _assert_bitexact(got, ref, "refinement under kernel timing")
+    _assert_bitexact(got2, ref, "refinement under kernel timing (2nd call)")
+    assert n_lin == n_sor == 2 * p.var_refine_iters
+    assert ms_lin > 0 and ms_sor > 0

@@ -73,6 +73,22 @@ def run(name, W, H, preset, B, steps, warmup, paper=0, fma=0):
         eng.calc_device(B, d0.data_ptr(), d1.data_ptr(), out.data_ptr(), s.cuda_stream)
     torch.cuda.synchronize()
     n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
+    refine = None
+    if p.var_refine_iters > 0:
+        # the finest level's refinement launches (HIP events, eager under timing),
+        # against an algorithmic-bytes model per pixel and fixed-point iteration
+        # (DESIGN.md 3b): linearisation reads the flow (8 B), I1 (4, the warp's
+        # taps once), I0 (4), I0x / I0y (8) and writes B1, B2, A12, D1, D2, the
+        # smoothness weight (24): 48 B; the SOR reads those 6 planes (24) and
+        # reads + writes the flow (16): 40 B
+        px = wl["padded_width"] * wl["padded_height"] // (4 ** p.finest_scale) * B
+        refine = {"level_pixels": px, "fixed_point_iterations": p.var_refine_iters}
+        for kname, kind, bpp in (("k_vr_lin", disflow.KERNEL_VR_LIN, 48), ("k_vr_sor", disflow.KERNEL_VR_SOR, 40)):
+            n_k, ms_k = eng.kernel_time(kind)
+            avg = ms_k / max(n_k, 1)
+            refine[kname] = {"launches": n_k, "avg_launch_ms": avg, "algorithmic_bytes_per_px": bpp,
+                            "achieved_GBps": bpp * px / (avg * 1e-3) / 1e9,
+                            "hbm_frac": bpp * px / (avg * 1e-3) / 8e12}
     eng.set_kernel_timing(False)
     launch_ms = ms_f / max(n_f, 1)
     flops = wl["search_flops_finest"] * B
@@ -89,6 +105,7 @@ def run(name, W, H, preset, B, steps, warmup, paper=0, fma=0):
                                                         "var_refine_iters": p.var_refine_iters,
                                                         "paper_mode": p.paper_mode},
             "batch": B, "steps": steps, "ms_per_step": el / steps * 1e3, "pairs_per_s": B * steps / el,
+            "refinement_finest_level": refine,
             "patches_per_pair": wl["patches"], "updates_per_pair": wl["updates"],
             "updates_per_s": wl["updates"] * B * steps / el}
 
