@@ -476,6 +476,11 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     __shared__ int2 cr[kOutSW], rr[kOutSH];
     __shared__ float s1[kPaper ? kPaperStage<UPSAMPLE> : 1];  // paper mode: staged I1 (see below)
     __shared__ int pbox[4];
+    // paper mode: window columns / rows sorted by their covering-patch count,
+    // and per column class v (count v): first pixel index, first sorted
+    // column, columns, RCP(columns) bits (see the densify loop)
+    __shared__ unsigned char csort[kPaper ? kOutSW : 1], rsort[kPaper ? kOutSH : 1];
+    __shared__ int4 ctab[K + 1];
     const int tid = threadIdx.x;
     const int ox = blockIdx.x * kOutTW, oy = blockIdx.y * kOutTH;
     const int pair = blockIdx.z;
@@ -547,6 +552,57 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                                   min(floordiv_r(py - a.offh + hp, rst), hb) - ha);
     }
     __syncthreads();
+    // paper mode: sort the window's columns (wave 0) and rows (wave 1) by
+    // covering-patch count, a stable counting sort by ballots. The densify
+    // below walks the window class by class, so the lanes of a wave share
+    // their counts and the K x K vote loop skips the empty slots wave-wide
+    // (unsorted, a wave's lanes mix the counts 2 and 3 of steps 3 and every
+    // lane issued all 9 slots for 7.1 votes on average).
+    if constexpr (kPaper) {
+        if (tid < 128) {
+            const bool cols = tid < 64;
+            const int n = cols ? rw : rh, lane = tid & 63;
+            unsigned char* out = cols ? csort : rsort;
+            auto cls = [&](int i) {
+                if (i >= n) return -1;
+                const int2 e = cols ? cr[i] : rr[i];
+                return max(e.y - e.x + 1, 0);
+            };
+            int cnt[K + 1];
+#pragma unroll
+            for (int v = 0; v <= K; ++v) cnt[v] = 0;
+            for (int b = 0; b < n; b += 64) {
+                const int v = cls(b + lane);
+#pragma unroll
+                for (int w = 0; w <= K; ++w) cnt[w] += __popcll(__ballot(v == w));
+            }
+            int base[K + 1];
+            base[0] = 0;
+#pragma unroll
+            for (int v = 1; v <= K; ++v) base[v] = base[v - 1] + cnt[v - 1];
+            if (cols && lane <= K) {
+                int b0 = 0, c0 = 0;
+#pragma unroll
+                for (int v = 0; v <= K; ++v)
+                    if (v == lane) {
+                        b0 = base[v];
+                        c0 = cnt[v];
+                    }
+                ctab[lane] = make_int4(b0 * rh, b0, c0, __float_as_int(__builtin_amdgcn_rcpf((float)max(c0, 1))));
+            }
+            for (int b = 0; b < n; b += 64) {
+                const int v = cls(b + lane);
+#pragma unroll
+                for (int w = 0; w <= K; ++w) {
+                    const unsigned long long m = __ballot(v == w);
+                    if (v == w)
+                        out[base[w] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                            (unsigned char)(b + lane);
+                    base[w] += __popcll(m);
+                }
+            }
+        }
+    }
     // paper mode: every vote samples I1 (bilinear, replicate border) at
     // X = clamp(RN(x + u.x), -1, W) for a window pixel x and a staged patch's
     // u, so its taps floor(X), floor(X) + 1 lie in [max(i0 + floor(min u.x),
@@ -592,9 +648,27 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         __syncthreads();
     }
     const float sc = a.sc;
-    const float rrw = __builtin_amdgcn_rcpf((float)rw);  // k / rw by floordiv_r: exact for k < 2^12
+    const float rrw = __builtin_amdgcn_rcpf((float)rw);  // k / rw by floordiv_r (exact, |k| < 2^20)
+    int pxc[K + 1];  // paper mode: first pixel index of each column class
+#pragma unroll
+    for (int v = 0; v <= K; ++v) pxc[v] = kPaper ? ctab[v].x : 0;
     for (int k = tid; k < rw * rh; k += 256) {
-        const int r = floordiv_r(k, rrw), c = k - r * rw;
+        int r, c;
+        if constexpr (kPaper) {
+            // pixel k of the class-major order: class z (the last whose first
+            // index <= k), then sorted row / sorted column within the class
+            int z = 0;
+#pragma unroll
+            for (int v = 1; v <= K; ++v) z += k >= pxc[v] ? 1 : 0;
+            const int4 e = ctab[z];
+            const int l = k - e.x;
+            const int rs = floordiv_r(l, __int_as_float(e.w));
+            c = csort[e.y + l - rs * e.z];
+            r = rsort[rs];
+        } else {
+            r = floordiv_r(k, rrw);
+            c = k - r * rw;
+        }
         // dense value: contributions in patch-id order, f from +0; masked
         // terms add +0, an exact no-op (f is never -0)
         const int2 xr = cr[c], yr = rr[r];

@@ -604,15 +604,43 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             const float i0v = I0c[(size_t)y * cW + x];
             const int2 xr = crng[gx - bgx0], yr = crng[BX + gy - bgy0];
             float fx = 0.0f, fy = 0.0f, wt = 0.0f;
-            for (int cx = xr.x; cx <= xr.y; ++cx)
-                for (int cy = yr.x; cy <= yr.y; ++cy) {
-                    const float2 v = cu[cx * PH + cy];
-                    const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
-                    const float c = recip_max1(d);  // correctly rounded (dis_device.h)
-                    fx = fx + c * v.x;
-                    fy = fy + c * v.y;
-                    wt = wt + c;
+            if constexpr (LPP == 2) {
+                // the patch's two lanes split the votes (vote t = 2m + q, patch-id
+                // order t = (cx - xr.x) * ny + cy - yr.x): each samples and weighs
+                // its own, then both add the pair's terms in vote order
+                const int ny = yr.y - yr.x + 1, n = max(xr.y - xr.x + 1, 0) * max(ny, 0);
+                const float rny = __builtin_amdgcn_rcpf((float)max(ny, 1));
+                for (int m = 0; 2 * m < n; ++m) {
+                    const int t = 2 * m + q;
+                    float c = 0.0f, cvx = 0.0f, cvy = 0.0f;
+                    if (t < n) {
+                        const int i = floordiv_r(t, rny);
+                        const float2 v = cu[(xr.x + i) * PH + yr.x + t - i * ny];
+                        const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
+                        c = recip_max1(d);  // correctly rounded (dis_device.h)
+                        cvx = c * v.x;
+                        cvy = c * v.y;
+                    }
+                    fx = fx + quad_perm<kQuadEven>(cvx);
+                    fy = fy + quad_perm<kQuadEven>(cvy);
+                    wt = wt + quad_perm<kQuadEven>(c);
+                    if (2 * m + 1 < n) {
+                        fx = fx + quad_perm<kQuadOdd>(cvx);
+                        fy = fy + quad_perm<kQuadOdd>(cvy);
+                        wt = wt + quad_perm<kQuadOdd>(c);
+                    }
                 }
+            } else {
+                for (int cx = xr.x; cx <= xr.y; ++cx)
+                    for (int cy = yr.x; cy <= yr.y; ++cy) {
+                        const float2 v = cu[cx * PH + cy];
+                        const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
+                        const float c = recip_max1(d);  // correctly rounded (dis_device.h)
+                        fx = fx + c * v.x;
+                        fy = fy + c * v.y;
+                        wt = wt + c;
+                    }
+            }
             if (wt > 0) {
                 fx = fx / wt;
                 fy = fy / wt;

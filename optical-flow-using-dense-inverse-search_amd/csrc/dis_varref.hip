@@ -53,6 +53,23 @@ __device__ __forceinline__ float* plane(const Lvl& L, int pair, int k)
     return L.ws + (size_t)pair * L.ws_stride + (size_t)k * L.ws_plane;
 }
 
+// XCD-aware tile order (as k_pyramid): the dispatcher deals linear block ids
+// round-robin to the 8 XCDs; remapped, each XCD walks a contiguous run of
+// tiles, so the halos that neighbouring tiles share are fetched into one L2
+struct Tile {
+    int x, y, z;
+};
+__device__ __forceinline__ Tile xcd_tile()
+{
+    const int nbx = gridDim.x, nby = gridDim.y;
+    const int nb = nbx * nby * gridDim.z;
+    const int lin = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    const int per = nb / 8;
+    const int t = (lin < per * 8) ? (lin % 8) * per + lin / 8 : lin;
+    return Tile{__builtin_amdgcn_readfirstlane(t % nbx), __builtin_amdgcn_readfirstlane((t / nbx) % nby),
+                __builtin_amdgcn_readfirstlane(t / (nbx * nby))};
+}
+
 // 5-tap derivative (1, -8, 0, 8, -1) / 12 of the taps a..d at -2, -1, +1, +2
 __device__ __forceinline__ float d5(float a, float b, float c, float d)
 {
@@ -94,6 +111,9 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
     __shared__ float sI[kFH][kFW];
     __shared__ float sWx[kGH][kGW], sWy[kGH][kGW], sGx[kGH][kGW], sGy[kGH][kGW];
     __shared__ float sS[kSH][kSW];
+    // (plain block order: the XCD-aware order halves this kernel's HBM reads,
+    // 904 -> 406 MB per 4K level-0 launch, but measured 3 x 33 us slower per
+    // config-5 step)
     const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
     const int x0 = blockIdx.x * kLW, y0 = blockIdx.y * kLH;
     const float* I0 = L.img0 + (size_t)pr * L.plane_stride;
@@ -258,11 +278,11 @@ static_assert(kSHY >= 2 * kVarRefSor - 1 && kSHX >= 2 * kVarRefSor - 1, "SOR hal
 // r1, r2 = RN(1 / d1), RN(1 / d2): each of the pixel's 5 updates divides by
 // the same d1, d2, so the division is div_pre (correctly rounded from the
 // reciprocal, dis_device.h) instead of the IEEE sequence; numerators below
-// 2^-60 (whose remainders could leave the normal range) take IEEE division
-// (The pixel's own du, dv live only in LDS, read back per update: the
-// reciprocals then fit the 128 VGPRs of 4 waves per SIMD.)
+// 2^-60 (whose remainders could leave the normal range) take IEEE division.
+// The left smoothness weight is the left pixel's own (its s), which the lane
+// holds (odd pixel) or lane q - 1 holds (even pixel), so it is not stored.
 struct SorPx {
-    float b1, b2, a12, d1, d2, r1, r2, s, sl, su;
+    float b1, b2, a12, d1, d2, r1, r2, s, su;
 };
 
 __device__ __forceinline__ float sor_div(float a, float b, float r)
@@ -271,6 +291,27 @@ __device__ __forceinline__ float sor_div(float a, float b, float r)
     return div_pre(a, b, r);
 }
 
+// lane q - 1's / q + 1's value (DPP wave shifts); 0 past the wave's ends,
+// which is the region's zero border
+__device__ __forceinline__ float from_left(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, true));  // wave_shr:1
+}
+__device__ __forceinline__ float from_right(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, true));  // wave_shl:1
+}
+
+// One wave per region row (rows wv + 16 j), lane q = pixel pair (2q, 2q + 1):
+// a pixel's left / right neighbours are in the same wave, so du, dv live in
+// registers and reach the neighbours by DPP; only the rows above / below go
+// through LDS (sU / sV, written after each update, read after the barrier).
+// A region row at distance d from the tile's rows matters for the tile after
+// the last half-sweep only while (half-sweep index h, 1-based) + d <= 2 *
+// VR_SOR: a row skipped at half-sweep h is wrong afterwards, and that reaches
+// the tile at half-sweep h + d. Skipping the rows past that (wave-uniform)
+// leaves every value the tile depends on as it was; the rest of the halo is
+// wrong either way.
 // kInt: every pixel of the region and its 4 neighbours inside the image (no
 // border masks; most tiles of a level)
 template <bool kInt>
@@ -279,6 +320,7 @@ __device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][
 {
     const int W = L.W, H = L.H;
     SorPx P[kSRows][2];
+    float U[kSRows][2], V[kSRows][2];
     const float* B1 = plane(L, pr, P_B1);
     const float* B2 = plane(L, pr, P_B2);
     const float* A12 = plane(L, pr, P_A12);
@@ -295,7 +337,8 @@ __device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][
             const bool in = kInt || (x >= 0 && x < W && y >= 0 && y < H);
             p.b1 = p.b2 = p.a12 = 0.0f;
             p.d1 = p.d2 = 1.0f;
-            p.s = p.sl = p.su = 0.0f;
+            p.s = p.su = 0.0f;
+            U[j][c] = V[j][c] = 0.0f;
             if (in) {
                 const size_t i = (size_t)y * W + x;
                 p.b1 = B1[i];
@@ -304,7 +347,6 @@ __device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][
                 p.d1 = D1[i];
                 p.d2 = D2[i];
                 p.s = SW[i];
-                p.sl = (kInt || x > 0) ? SW[i - 1] : 0.0f;
                 p.su = (kInt || y > 0) ? SW[i - W] : 0.0f;
             }
         }
@@ -320,35 +362,45 @@ __device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][
     for (int sweep = 0; sweep < kVarRefSor; ++sweep) {
 #pragma unroll
         for (int colour = 0; colour < 2; ++colour) {
+            const int h = 2 * sweep + colour + 1;
 #pragma unroll
             for (int j = 0; j < kSRows; ++j) {
-                const int r = wv + kSWaves * j;  // region row
+                const int r = wv + kSWaves * j;  // region row (wave-uniform)
+                const int d = max(max(kSHY - r, r - (kSHY + kSTH - 1)), 0);
+                if (h + d > 2 * kVarRefSor) continue;
                 const int y = ys + r;
                 // the pixel of this colour in the pair: x parity = c, (x + y) & 1 == colour
-                const int cpar = (colour ^ y) & 1;  // wave-uniform
+                const int cpar = (colour ^ y) & 1;
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     if (c != cpar) continue;
-                    SorPx& p = P[j][c];
+                    const SorPx& p = P[j][c];
                     const int x = xs + 2 * q + c;
-                    if (!kInt && !(x >= 0 && x < W && y >= 0 && y < H)) continue;
+                    const bool in = kInt || (x >= 0 && x < W && y >= 0 && y < H);
                     const bool hl = kInt || x > 0, hr = kInt || x < W - 1, hu = kInt || y > 0, hd = kInt || y < H - 1;
-                    const float wl = hl ? p.sl : 0.0f, wr = hr ? p.s : 0.0f;
+                    const float du = U[j][c], dv = V[j][c];
+                    // same row: the pair's other pixel and the neighbouring pair's
+                    const float ul0 = c == 0 ? from_left(U[j][1]) : U[j][0];
+                    const float ur0 = c == 0 ? U[j][1] : from_right(U[j][0]);
+                    const float vl0 = c == 0 ? from_left(V[j][1]) : V[j][0];
+                    const float vr0 = c == 0 ? V[j][1] : from_right(V[j][0]);
+                    const float sl = c == 0 ? from_left(P[j][1].s) : P[j][0].s;
+                    const float wl = hl ? sl : 0.0f, wr = hr ? p.s : 0.0f;
                     const float wu = hu ? p.su : 0.0f, wd = hd ? p.s : 0.0f;
-                    const float du = sU[c][r + 1][q + 1], dv = sV[c][r + 1][q + 1];
-                    // neighbours (other parity): same row left / right, rows above / below same parity
-                    const int o = 1 - c;
-                    const int ql = c == 0 ? q : q + 1, qr = c == 0 ? q + 1 : q + 2;
-                    const float ul = hl ? sU[o][r + 1][ql] : du, ur = hr ? sU[o][r + 1][qr] : du;
+                    const float ul = hl ? ul0 : du, ur = hr ? ur0 : du;
                     const float uu = hu ? sU[c][r][q + 1] : du, ud = hd ? sU[c][r + 2][q + 1] : du;
-                    const float vl = hl ? sV[o][r + 1][ql] : dv, vr = hr ? sV[o][r + 1][qr] : dv;
+                    const float vl = hl ? vl0 : dv, vr = hr ? vr0 : dv;
                     const float vu = hu ? sV[c][r][q + 1] : dv, vd = hd ? sV[c][r + 2][q + 1] : dv;
                     const float sdu = ((wl * ul + wr * ur) + wu * uu) + wd * ud;
                     const float nu = (1.0f - kOmega) * du + kOmega * sor_div((p.b1 + sdu) - p.a12 * dv, p.d1, p.r1);
                     const float sdv = ((wl * vl + wr * vr) + wu * vu) + wd * vd;
                     const float nv = (1.0f - kOmega) * dv + kOmega * sor_div((p.b2 + sdv) - p.a12 * nu, p.d2, p.r2);
-                    sU[c][r + 1][q + 1] = nu;
-                    sV[c][r + 1][q + 1] = nv;
+                    // pixels outside the image keep du = dv = 0 (their cells are never read as
+                    // neighbours: the border masks above select the pixel itself)
+                    U[j][c] = in ? nu : du;
+                    V[j][c] = in ? nv : dv;
+                    sU[c][r + 1][q + 1] = U[j][c];
+                    sV[c][r + 1][q + 1] = V[j][c];
                 }
             }
             __syncthreads();
@@ -367,7 +419,7 @@ __device__ __forceinline__ void sor_tile(const Lvl& L, float (&sU)[2][kSRH + 2][
             if (lx < 0 || lx >= kSTW || (!kInt && !(x >= 0 && x < W && y >= 0 && y < H))) continue;
             float2* f = fl + (size_t)y * W + x;
             const float2 v = *f;
-            *f = make_float2(v.x + sU[c][r + 1][q + 1], v.y + sV[c][r + 1][q + 1]);
+            *f = make_float2(v.x + U[j][c], v.y + V[j][c]);
         }
     }
 }
@@ -376,9 +428,10 @@ __global__ void __launch_bounds__(1024) k_vr_sor(Lvl L)
 {
     // [column parity][region row + 1][pair + 1]; border cells stay 0
     __shared__ float sU[2][kSRH + 2][kSQ + 2], sV[2][kSRH + 2][kSQ + 2];
-    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
+    const Tile bt = xcd_tile();
+    const int W = L.W, H = L.H, pr = bt.z, tid = threadIdx.x;
     const int q = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = blockIdx.x * kSTW, y0 = blockIdx.y * kSTH;
+    const int x0 = bt.x * kSTW, y0 = bt.y * kSTH;
     const int xs = x0 - kSHX, ys = y0 - kSHY;  // xs even
     for (int k = tid; k < 2 * (kSRH + 2) * (kSQ + 2); k += 1024) {
         (&sU[0][0][0])[k] = 0.0f;
