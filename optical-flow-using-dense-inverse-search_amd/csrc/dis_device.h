@@ -27,15 +27,17 @@ __device__ __forceinline__ int floordiv_r(int a, float rb)
     return (int)floorf(((float)a + 0.5f) * rb);
 }
 
-// Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
-// (src/patch.cpp:176): pivot on |a10| > |a00| (first index wins ties),
-// l = a_q0 / a_p0 (skipped when the pivot is 0), u11 = a_q1 - l * a_p1.
+// fminf(fmaxf(v, -1), hi) in one v_med3_f32 (a selection: same value for
+// every non-NaN v, which is all the callers pass -- sample positions x + u of
+// finite flows; fmaxf's NaN handling cost a canonicalising max besides)
+__device__ __forceinline__ float clamp_m1(float v, float hi) { return __builtin_amdgcn_fmed3f(v, -1.0f, hi); }
+
 // I1 sampled at (X, Y): bilinear, replicate border; the position is first
 // clamped to [-1, W] x [-1, H] (oracle vr_warp: identical expressions).
 __device__ __forceinline__ float bilinear_replicate(const float* __restrict__ I, int W, int H, float X, float Y)
 {
-    X = fminf(fmaxf(X, -1.0f), (float)W);
-    Y = fminf(fmaxf(Y, -1.0f), (float)H);
+    X = clamp_m1(X, (float)W);
+    Y = clamp_m1(Y, (float)H);
     const float fx0 = floorf(X), fy0 = floorf(Y);
     const int xa = (int)fx0, ya = (int)fy0;
     const float fx = X - fx0, fy = Y - fy0;
@@ -49,6 +51,9 @@ __device__ __forceinline__ float bilinear_replicate(const float* __restrict__ I,
     return (1.0f - fy) * top + fy * bot;
 }
 
+// Pre-factored Eigen PartialPivLU of the fixed 2x2 patch Hessian
+// (src/patch.cpp:176): pivot on |a10| > |a00| (first index wins ties),
+// l = a_q0 / a_p0 (skipped when the pivot is 0), u11 = a_q1 - l * a_p1.
 struct LU2 {
     float u00, u01, l10, u11;
     int swap;

@@ -536,6 +536,27 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             if (tid + 256 * j < kOutPX * kOutPY)
                 pu[tid + 256 * j] = kPaper ? v[j] : make_float2(v[j].x * 0.5f, v[j].y * 0.5f);
     }
+    if constexpr (kPaper) {
+        // I0 of the window, parked in the .x of each pixel's dense slot (the
+        // pixel's densify reads it there before writing the slot), the loads
+        // issued together with the patch staging's
+        constexpr int NW = (kOutSW * kOutSH + 255) / 256;
+        const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
+        const float rrw0 = __builtin_amdgcn_rcpf((float)rw);
+        float v0[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            const int k = tid + 256 * j;
+            const int r = floordiv_r(k, rrw0), c = k - r * rw;
+            v0[j] = k < rw * rh ? I0[(size_t)(j0 + r) * a.wF + i0 + c] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            const int k = tid + 256 * j;
+            const int r = floordiv_r(k, rrw0), c = k - r * rw;
+            if (k < rw * rh) dense[r * kOutSW + c].x = v0[j];
+        }
+    }
     if (!kPaper && tid >= 64 && tid - 64 <= K * K) {
         const int n = tid - 64;
         rtab[n] = n ? 1.0f / (0.5f * (float)n) : 0.0f;
@@ -636,13 +657,22 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             sws = bx1 - bx0 + 1;
             const int shs = by1 - by0 + 1;
             staged = sws > 0 && shs > 0 && sws * shs <= kPaperStage<UPSAMPLE>;
-            if (staged) {
+            if (staged) {  // every load issued before the first store: one memory latency
+                constexpr int NS = (kPaperStage<UPSAMPLE> + 255) / 256;
                 const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
                 const float rsw = __builtin_amdgcn_rcpf((float)sws);
-                for (int k = tid; k < sws * shs; k += 256) {
+                const int n1 = sws * shs;
+                float v1[NS];
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    const int k = tid + 256 * j;
                     const int r = floordiv_r(k, rsw), c = k - r * sws;
-                    s1[k] = I1[(size_t)clampi(by0 + r, 0, a.hF - 1) * a.wF + clampi(bx0 + c, 0, a.wF - 1)];
+                    v1[j] = k < n1 ? I1[(size_t)clampi(by0 + r, 0, a.hF - 1) * a.wF + clampi(bx0 + c, 0, a.wF - 1)]
+                                   : 0.0f;
                 }
+#pragma unroll
+                for (int j = 0; j < NS; ++j)
+                    if (tid + 256 * j < n1) s1[tid + 256 * j] = v1[j];
             }
         }
         __syncthreads();
@@ -676,9 +706,8 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         if constexpr (kPaper) {
             // SURVEY 8f row 4 (oracle densify_paper): weight 1/max(1, |I1(x+u) - I0(x)|)
             const int xg = i0 + c, yg = j0 + r;  // level-F pixel
-            const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
             const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
-            const float i0v = I0[(size_t)yg * a.wF + xg];
+            const float i0v = dense[r * kOutSW + c].x;  // I0(x), staged above
             const float xf = (float)xg, yf = (float)yg;
 #pragma unroll
             for (int i = 0; i < K; ++i)
@@ -688,8 +717,8 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                         const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
                         float d;
                         if (staged) {  // bilinear_replicate's expressions on the staged taps
-                            const float X = fminf(fmaxf(xf + t.x, -1.0f), (float)a.wF);
-                            const float Y = fminf(fmaxf(yf + t.y, -1.0f), (float)a.hF);
+                            const float X = clamp_m1(xf + t.x, (float)a.wF);
+                            const float Y = clamp_m1(yf + t.y, (float)a.hF);
                             const float fx0 = floorf(X), fy0 = floorf(Y);
                             const float ax = X - fx0, ay = Y - fy0;
                             const float* q = s1 + __mul24((int)fy0 - by0, sws) + ((int)fx0 - bx0);
