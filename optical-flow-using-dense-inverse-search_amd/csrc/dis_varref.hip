@@ -70,10 +70,22 @@ __device__ __forceinline__ Tile xcd_tile()
                 __builtin_amdgcn_readfirstlane(t / (nbx * nby))};
 }
 
-// 5-tap derivative (1, -8, 0, 8, -1) / 12 of the taps a..d at -2, -1, +1, +2
+// a / b correctly rounded from r = RN(1 / b) (div_pre, dis_device.h);
+// numerators below 2^-60 (whose remainders could leave the normal range) take
+// IEEE division
+__device__ __forceinline__ float sor_div(float a, float b, float r)
+{
+    if (a != 0.0f && fabsf(a) < 0x1p-60f) return a / b;
+    return div_pre(a, b, r);
+}
+
+// 5-tap derivative (1, -8, 0, 8, -1) / 12 of the taps a..d at -2, -1, +1, +2;
+// the division by 12 from the folded RN(1 / 12) (~6 instructions instead of
+// the ~10 of the IEEE sequence; 8.5 of them per pixel in k_vr_lin)
+constexpr float kR12 = 1.0f / 12.0f;
 __device__ __forceinline__ float d5(float a, float b, float c, float d)
 {
-    return (((a - 8.0f * b) + 8.0f * c) - d) / 12.0f;
+    return sor_div(((a - 8.0f * b) + 8.0f * c) - d, 12.0f, kR12);
 }
 
 // I0x, I0y of the level (replicate border), once per level; 2-D grid
@@ -95,8 +107,11 @@ __global__ void __launch_bounds__(256) k_vr_d0(Lvl L)
 
 // ---------------------------------------------------------------------------
 // linearisation
-constexpr int kLW = 64, kLH = 16;             // output tile
-constexpr int kFW = kLW + 8, kFH = kLH + 8;   // flow, warped I1: tile +-4
+// 32 x 32 output tiles and the flow kept only over the tile +-1 (the warp's
+// +-4 halo lives in registers until sI is formed): 40.7 KB of LDS, 4
+// workgroups per CU (64 x 16 tiles with the flow staged over +-4: 47 KB, 3)
+constexpr int kLW = 32, kLH = 32;             // output tile
+constexpr int kFW = kLW + 8, kFH = kLH + 8;   // flow loads, warped I1: tile +-4
 constexpr int kGW = kLW + 4, kGH = kLH + 4;   // Wx, Wy, I0x, I0y: tile +-2
 constexpr int kSW = kLW + 1, kSH = kLH + 1;   // smoothness weight: tile + left column, top row
 
@@ -107,7 +122,7 @@ constexpr int kSW = kLW + 1, kSH = kLH + 1;   // smoothness weight: tile + left 
 // c +- 1, 2 -- each of which again holds the value at the clamped position.
 __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
 {
-    __shared__ float2 sF[kFH][kFW];
+    __shared__ float2 sF[kLH + 2][kLW + 2];  // the flow over the tile +-1
     __shared__ float sI[kFH][kFW];
     __shared__ float sWx[kGH][kGW], sWy[kGH][kGW], sGx[kGH][kGW], sGy[kGH][kGW];
     __shared__ float sS[kSH][kSW];
@@ -175,7 +190,7 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
         if (k >= kFW * kFH) break;
         const int ly = k / kFW, lx = k - ly * kFW;
         const float fx = wfx[t], fy = wfy[t];
-        sF[ly][lx] = f[t];
+        if (ly >= 3 && ly < kLH + 5 && lx >= 3 && lx < kLW + 5) sF[ly - 3][lx - 3] = f[t];
         const float top = (1.0f - fx) * ta[t] + fx * tb[t];
         const float bot = (1.0f - fx) * tc[t] + fx * td[t];
         sI[ly][lx] = (1.0f - fy) * top + fy * bot;
@@ -202,7 +217,7 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
         const int ly = k / kSW, lx = k - ly * kSW;
         const int x = x0 - 1 + lx, y = y0 - 1 + ly;
         if (x < 0 || y < 0 || x >= W || y >= H) continue;  // never read
-        const int fx = lx + 3, fy = ly + 3;
+        const int fx = lx, fy = ly;  // sF index of (x, y)
         const float uc = sF[fy][fx].x, vc = sF[fy][fx].y;
         float gxu = 0.0f, gxv = 0.0f, gyu = 0.0f, gyv = 0.0f;
         if (x < W - 1) {
@@ -224,12 +239,12 @@ __global__ void __launch_bounds__(256) k_vr_lin(Lvl L)
         const int ly = k / kLW, lx = k - ly * kLW;
         const int x = x0 + lx, y = y0 + ly;
         if (x >= W || y >= H) continue;
-        const int gx = lx + 2, gy = ly + 2, fx = lx + 4, fy = ly + 4;
+        const int gx = lx + 2, gy = ly + 2, fx = lx + 1, fy = ly + 1;
         const size_t i = (size_t)y * W + x;
         const float wx = sWx[gy][gx], wy = sWy[gy][gx], i0x = sGx[gy][gx], i0y = sGy[gy][gx];
         const float Ix = 0.5f * (wx + i0x);
         const float Iy = 0.5f * (wy + i0y);
-        const float Iz = sI[fy][fx] - i0p[t];
+        const float Iz = sI[ly + 4][lx + 4] - i0p[t];
         const float Ixx = 0.5f * (d5(sWx[gy][gx - 2], sWx[gy][gx - 1], sWx[gy][gx + 1], sWx[gy][gx + 2]) +
                                   d5(sGx[gy][gx - 2], sGx[gy][gx - 1], sGx[gy][gx + 1], sGx[gy][gx + 2]));
         const float Ixy = 0.5f * (d5(sWx[gy - 2][gx], sWx[gy - 1][gx], sWx[gy + 1][gx], sWx[gy + 2][gx]) +
@@ -284,12 +299,6 @@ static_assert(kSHY >= 2 * kVarRefSor - 1 && kSHX >= 2 * kVarRefSor - 1, "SOR hal
 struct SorPx {
     float b1, b2, a12, d1, d2, r1, r2, s, su;
 };
-
-__device__ __forceinline__ float sor_div(float a, float b, float r)
-{
-    if (a != 0.0f && fabsf(a) < 0x1p-60f) return a / b;
-    return div_pre(a, b, r);
-}
 
 // lane q - 1's / q + 1's value (DPP wave shifts); 0 past the wave's ends,
 // which is the region's zero border
