@@ -555,16 +555,17 @@ def test_pyramid_sqrt_is_correctly_rounded_on_every_input():
 
 @pytest.mark.gpu
 def test_colour_fast_division_and_sqrt_are_ieee():
-    # dis_color.hip's fast cores (dis_device.h div_core / sqrt_core) rest on
-    # this GPU's v_rcp_f32 / v_sqrt_f32 seeds: tools/color_core_check compares
-    # them with IEEE a / b and sqrtf on every divisor mantissa and on whole
-    # binades of the sqrt domain
+    # dis_color.hip's fast cores (dis_device.h div_core / sqrt_core) and the
+    # paper mode's reciprocal (recip_core) rest on this GPU's v_rcp_f32 /
+    # v_sqrt_f32 seeds: tools/color_core_check compares them with IEEE a / b,
+    # sqrtf and 1.0f / m on every divisor mantissa, whole binades of the sqrt
+    # domain and every float of the reciprocal's domain
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "color_core_check")
     assert os.path.exists(exe), "tools/color_core_check not built (__graft_entry__.build)"
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0 and out.stdout.count("mismatches 0") == 8, out.stdout + out.stderr
+    assert out.returncode == 0 and out.stdout.count("mismatches 0") == 9, out.stdout + out.stderr
 
 
 def test_medium_4k_batch_bitexact(disflow_mod, oracle):

@@ -7,6 +7,8 @@
 //    [b 2^-30, b] (the powers of two and hashed mantissas, both edges), plus
 //    the same at divisor exponents -60, -31, 30, 59 for every 16th mantissa;
 //  sqrt: every x in [1, 4), [2^-96, 2^-94) and [2^94, 2^96) (2^24 each);
+//  reciprocal (recip_core, the paper mode's vote weights): every m in
+//    [1, 2^30) (30 x 2^23 floats);
 // each against the compiler's IEEE a / b and sqrtf. Prints counts; exit 1 on
 // a mismatch.  hipcc --offload-arch=gfx950 -O3 -ffp-contract=off
 #include <hip/hip_runtime.h>
@@ -59,6 +61,17 @@ __global__ void k_sqrt(int exp0, unsigned long long* bad, unsigned int* first)
     }
 }
 
+__global__ void k_recip(unsigned long long* bad, unsigned int* first)
+{
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;  // 30 binades from 1
+    if (i >= 30u << 23) return;
+    const float m = __uint_as_float((127u << 23) + i);
+    if (__float_as_uint(dis::recip_core(m)) != __float_as_uint(1.0f / m)) {
+        atomicAdd(bad, 1ull);
+        atomicMin(first, i);
+    }
+}
+
 int main()
 {
     unsigned long long* bad;
@@ -87,5 +100,6 @@ int main()
         snprintf(name, sizeof name, "sqrt x in [2^%d, 2^%d)", e, e + 2);
         run(name, [&] { hipLaunchKernelGGL(k_sqrt, dim3((1 << 24) / 256), dim3(256), 0, 0, e, bad, first); });
     }
+    run("recip m in [1, 2^30)", [&] { hipLaunchKernelGGL(k_recip, dim3((30u << 23) / 256), dim3(256), 0, 0, bad, first); });
     return rc;
 }
