@@ -224,11 +224,14 @@ __device__ __forceinline__ float recip_core(float m)
 
 // 1 / max(1, |d|), correctly rounded (the paper mode's vote weight, Kroeger et
 // al. 2016 eq. 4): recip_core for m = max(1, |d|) < 2^30, the IEEE division
-// above that (and for NaN-free infinities)
+// above that (and for NaN-free infinities), behind a wave-uniform test (no
+// exec-mask bookkeeping while no lane needs it)
 __device__ __forceinline__ float recip_max1(float d)
 {
     const float m = fmaxf(1.0f, fabsf(d));
-    return m < 0x1p30f ? recip_core(m) : 1.0f / m;
+    const float y = recip_core(m);
+    if (__builtin_amdgcn_ballot_w64(!(m < 0x1p30f)) == 0) return y;
+    return m < 0x1p30f ? y : 1.0f / m;
 }
 
 // sqrtf(x), correctly rounded, for x = +0 or 2^-96 <= x <= 2^96 (sqrt_core_ok):

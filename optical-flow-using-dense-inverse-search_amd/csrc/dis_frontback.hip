@@ -402,9 +402,12 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 
 
 // paper mode: I1 of level F over every tap the window's weighted votes can
-// reach (floats; F == 0 has the twice wider window), staged when it fits
+// reach (floats; F == 0 has the twice wider window), staged when it fits, at a
+// fixed row stride (a vote's lower taps at constant LDS offsets)
 template <bool UPS>
 constexpr int kPaperStage = UPS ? 56 * 56 : 80 * 80;
+template <bool UPS>
+constexpr int kPaperSS = UPS ? 64 : 96;
 
 // one float4 (two output pixels) of the flow. (Streaming, non-temporal
 // stores made the one-stream kernel trace faster -- the next call's pyramid
@@ -656,23 +659,25 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const int bx1 = min(i1 + pbox[2] + 1, a.wF) + 1, by1 = min(j1 + pbox[3] + 1, a.hF) + 1;
             sws = bx1 - bx0 + 1;
             const int shs = by1 - by0 + 1;
-            staged = sws > 0 && shs > 0 && sws * shs <= kPaperStage<UPSAMPLE>;
+            staged = sws > 0 && shs > 0 && sws <= kPaperSS<UPSAMPLE> && shs * kPaperSS<UPSAMPLE> <= kPaperStage<UPSAMPLE>;
             if (staged) {  // every load issued before the first store: one memory latency
                 constexpr int NS = (kPaperStage<UPSAMPLE> + 255) / 256;
                 const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
                 const float rsw = __builtin_amdgcn_rcpf((float)sws);
                 const int n1 = sws * shs;
                 float v1[NS];
+                int at[NS];
 #pragma unroll
                 for (int j = 0; j < NS; ++j) {
                     const int k = tid + 256 * j;
                     const int r = floordiv_r(k, rsw), c = k - r * sws;
+                    at[j] = r * kPaperSS<UPSAMPLE> + c;
                     v1[j] = k < n1 ? I1[(size_t)clampi(by0 + r, 0, a.hF - 1) * a.wF + clampi(bx0 + c, 0, a.wF - 1)]
                                    : 0.0f;
                 }
 #pragma unroll
                 for (int j = 0; j < NS; ++j)
-                    if (tid + 256 * j < n1) s1[tid + 256 * j] = v1[j];
+                    if (tid + 256 * j < n1) s1[at[j]] = v1[j];
             }
         }
         __syncthreads();
@@ -682,93 +687,105 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     int pxc[K + 1];  // paper mode: first pixel index of each column class
 #pragma unroll
     for (int v = 0; v <= K; ++v) pxc[v] = kPaper ? ctab[v].x : 0;
-    for (int k = tid; k < rw * rh; k += 256) {
-        int r, c;
-        if constexpr (kPaper) {
-            // pixel k of the class-major order: class z (the last whose first
-            // index <= k), then sorted row / sorted column within the class
-            int z = 0;
+    // paper mode, staged: a tap's LDS index fma(floor Y, stride, floor X)
+    // (integers below 2^24: exact) from s1b = s1 - (by0 * stride + bx0)
+    constexpr int kSS = kPaperSS<UPSAMPLE>;
+    const float* s1b = s1 - (by0 * kSS + bx0);
+    // the staged / global choice (block-uniform) outside the pixel loop
+    auto densify = [&](auto staged_c) {
+        constexpr bool kStaged = decltype(staged_c)::value;
+        for (int k = tid; k < rw * rh; k += 256) {
+            int r, c;
+            if constexpr (kPaper) {
+                // pixel k of the class-major order: class z (the last whose first
+                // index <= k), then sorted row / sorted column within the class
+                int z = 0;
 #pragma unroll
-            for (int v = 1; v <= K; ++v) z += k >= pxc[v] ? 1 : 0;
-            const int4 e = ctab[z];
-            const int l = k - e.x;
-            const int rs = floordiv_r(l, __int_as_float(e.w));
-            c = csort[e.y + l - rs * e.z];
-            r = rsort[rs];
-        } else {
-            r = floordiv_r(k, rrw);
-            c = k - r * rw;
-        }
-        // dense value: contributions in patch-id order, f from +0; masked
-        // terms add +0, an exact no-op (f is never -0)
-        const int2 xr = cr[c], yr = rr[r];
-        float fx = 0.0f, fy = 0.0f, w = 0.0f;
-        if constexpr (kPaper) {
-            // SURVEY 8f row 4 (oracle densify_paper): weight 1/max(1, |I1(x+u) - I0(x)|)
-            const int xg = i0 + c, yg = j0 + r;  // level-F pixel
-            const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
-            const float i0v = dense[r * kOutSW + c].x;  // I0(x), staged above
-            const float xf = (float)xg, yf = (float)yg;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    if ((xr.x + i <= xr.y) && (yr.x + j <= yr.y)) {
-                        const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
-                        float d;
-                        if (staged) {  // bilinear_replicate's expressions on the staged taps
-                            const float X = clamp_m1(xf + t.x, (float)a.wF);
-                            const float Y = clamp_m1(yf + t.y, (float)a.hF);
-                            const float fx0 = floorf(X), fy0 = floorf(Y);
-                            const float ax = X - fx0, ay = Y - fy0;
-                            const float* q = s1 + __mul24((int)fy0 - by0, sws) + ((int)fx0 - bx0);
-                            const float top = (1.0f - ax) * q[0] + ax * q[1];
-                            const float bot = (1.0f - ax) * q[sws] + ax * q[sws + 1];
-                            d = ((1.0f - ay) * top + ay * bot) - i0v;
-                        } else {
-                            d = bilinear_replicate(I1, a.wF, a.hF, xf + t.x, yf + t.y) - i0v;
-                        }
-                        const float cw = recip_max1(d);  // correctly rounded (dis_device.h)
-                        fx = fx + cw * t.x;
-                        fy = fy + cw * t.y;
-                        w = w + cw;
-                    }
-                }
-        } else {
-            // covering patches per axis (<= K), read at constant offsets from the
-            // first one (the LDS array is padded for the taps past the range)
-            const int nx = max(xr.y - xr.x + 1, 0), ny = max(yr.y - yr.x + 1, 0);
-            const float2* pb = pu + xr.x * kOutPY + yr.x;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const bool ok = i < nx && j < ny;
-                    const float2 t = pb[i * kOutPY + j];
-                    fx = fx + (ok ? t.x : 0.0f);
-                    fy = fy + (ok ? t.y : 0.0f);
-                }
-            // the reference's weight sum of 0.5 per covering patch, exactly
-            const int n = nx * ny;
-            w = 0.5f * (float)n;
-            // fx / w correctly rounded from the tabulated RN(1 / w) (div_pre);
-            // tiny nonzero numerators, whose remainders could underflow, take
-            // the IEEE division below
-            const bool tiny = (fx != 0.0f && fabsf(fx) < 0x1p-100f) || (fy != 0.0f && fabsf(fy) < 0x1p-100f);
-            if (n > 0 && !tiny) {
-                const float rcp = rtab[n];
-                fx = div_pre(fx, w, rcp);
-                fy = div_pre(fy, w, rcp);
-                w = 0.0f;  // done
+                for (int v = 1; v <= K; ++v) z += k >= pxc[v] ? 1 : 0;
+                const int4 e = ctab[z];
+                const int l = k - e.x;
+                const int rs = floordiv_r(l, __int_as_float(e.w));
+                c = csort[e.y + l - rs * e.z];
+                r = rsort[rs];
+            } else {
+                r = floordiv_r(k, rrw);
+                c = k - r * rw;
             }
+            // dense value: contributions in patch-id order, f from +0; masked
+            // terms add +0, an exact no-op (f is never -0)
+            const int2 xr = cr[c], yr = rr[r];
+            float fx = 0.0f, fy = 0.0f, w = 0.0f;
+            if constexpr (kPaper) {
+                // SURVEY 8f row 4 (oracle densify_paper): weight 1/max(1, |I1(x+u) - I0(x)|)
+                const int xg = i0 + c, yg = j0 + r;  // level-F pixel
+                const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
+                const float i0v = dense[r * kOutSW + c].x;  // I0(x), staged above
+                const float xf = (float)xg, yf = (float)yg;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        if ((xr.x + i <= xr.y) && (yr.x + j <= yr.y)) {
+                            const float2 t = pu[(xr.x + i) * kOutPY + yr.x + j];
+                            float d;
+                            if constexpr (kStaged) {  // bilinear_replicate's expressions on the staged taps
+                                const float X = clamp_m1(xf + t.x, (float)a.wF);
+                                const float Y = clamp_m1(yf + t.y, (float)a.hF);
+                                const float fx0 = floorf(X), fy0 = floorf(Y);
+                                const float ax = X - fx0, ay = Y - fy0;
+                                const float* q = s1b + (int)__builtin_fmaf(fy0, (float)kSS, fx0);
+                                const float top = (1.0f - ax) * q[0] + ax * q[1];
+                                const float bot = (1.0f - ax) * q[kSS] + ax * q[kSS + 1];
+                                d = ((1.0f - ay) * top + ay * bot) - i0v;
+                            } else {
+                                d = bilinear_replicate(I1, a.wF, a.hF, xf + t.x, yf + t.y) - i0v;
+                            }
+                            const float cw = recip_max1(d);  // correctly rounded (dis_device.h)
+                            fx = fx + cw * t.x;
+                            fy = fy + cw * t.y;
+                            w = w + cw;
+                        }
+                    }
+            } else {
+                // covering patches per axis (<= K), read at constant offsets from the
+                // first one (the LDS array is padded for the taps past the range)
+                const int nx = max(xr.y - xr.x + 1, 0), ny = max(yr.y - yr.x + 1, 0);
+                const float2* pb = pu + xr.x * kOutPY + yr.x;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        const bool ok = i < nx && j < ny;
+                        const float2 t = pb[i * kOutPY + j];
+                        fx = fx + (ok ? t.x : 0.0f);
+                        fy = fy + (ok ? t.y : 0.0f);
+                    }
+                // the reference's weight sum of 0.5 per covering patch, exactly
+                const int n = nx * ny;
+                w = 0.5f * (float)n;
+                // fx / w correctly rounded from the tabulated RN(1 / w) (div_pre);
+                // tiny nonzero numerators, whose remainders could underflow, take
+                // the IEEE division below
+                const bool tiny = (fx != 0.0f && fabsf(fx) < 0x1p-100f) || (fy != 0.0f && fabsf(fy) < 0x1p-100f);
+                if (n > 0 && !tiny) {
+                    const float rcp = rtab[n];
+                    fx = div_pre(fx, w, rcp);
+                    fy = div_pre(fy, w, rcp);
+                    w = 0.0f;  // done
+                }
+            }
+            if (w > 0) {
+                fx = fx / w;
+                fy = fy / w;
+            }
+            // flowout *= sc_fct (src/main.cpp:194) before the resize
+            dense[r * kOutSW + c] = UPSAMPLE ? make_float2(fx * sc, fy * sc) : make_float2(fx, fy);
         }
-        if (w > 0) {
-            fx = fx / w;
-            fy = fy / w;
-        }
-        // flowout *= sc_fct (src/main.cpp:194) before the resize
-        dense[r * kOutSW + c] = UPSAMPLE ? make_float2(fx * sc, fy * sc) : make_float2(fx, fy);
-    }
+    };
+    if (kPaper && staged)
+        densify(std::true_type{});
+    else
+        densify(std::false_type{});
     __syncthreads();
 
     constexpr int RPT = kOutTH / 8;  // output rows per thread
