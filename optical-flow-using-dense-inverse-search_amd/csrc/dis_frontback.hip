@@ -403,11 +403,14 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 
 // paper mode: I1 of level F over every tap the window's weighted votes can
 // reach (floats; F == 0 has the twice wider window), staged when it fits, at a
-// fixed row stride (a vote's lower taps at constant LDS offsets)
+// fixed row stride (a vote's lower taps at constant LDS offsets). F >= 1:
+// 48 x 50 keeps the workgroup at 23 KB of LDS, 7 per CU (56 x 56: 26 KB, 6 per
+// CU, measured 6 % slower); a window whose flows spread wider than ~11 level-F
+// pixels reads I1 globally instead (same values)
 template <bool UPS>
-constexpr int kPaperStage = UPS ? 56 * 56 : 80 * 80;
+constexpr int kPaperStage = UPS ? 48 * 50 : 80 * 80;
 template <bool UPS>
-constexpr int kPaperSS = UPS ? 64 : 96;
+constexpr int kPaperSS = UPS ? 48 : 96;
 
 // one float4 (two output pixels) of the flow. (Streaming, non-temporal
 // stores made the one-stream kernel trace faster -- the next call's pyramid

@@ -610,24 +610,72 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
                 // its own, then both add the pair's terms in vote order
                 const int ny = yr.y - yr.x + 1, n = max(xr.y - xr.x + 1, 0) * max(ny, 0);
                 const float rny = __builtin_amdgcn_rcpf((float)max(ny, 1));
-                for (int m = 0; 2 * m < n; ++m) {
-                    const int t = 2 * m + q;
-                    float c = 0.0f, cvx = 0.0f, cvy = 0.0f;
-                    if (t < n) {
+                // up to 2 kPV votes (3 x 3 covering patches): every tap of the
+                // lane's votes loaded before the first is used (one memory
+                // latency instead of one per vote); a lane past n reloads the
+                // last vote and discards it
+                constexpr int kPV = 5;
+                if (n > 0 && n <= 2 * kPV) {
+                    float2 v[kPV];
+                    float tp[kPV][4], X[kPV], Y[kPV];
+#pragma unroll
+                    for (int m = 0; m < kPV; ++m) {
+                        const int t = min(2 * m + q, n - 1);
                         const int i = floordiv_r(t, rny);
-                        const float2 v = cu[(xr.x + i) * PH + yr.x + t - i * ny];
-                        const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
-                        c = recip_max1(d);  // correctly rounded (dis_device.h)
-                        cvx = c * v.x;
-                        cvy = c * v.y;
+                        v[m] = cu[(xr.x + i) * PH + yr.x + t - i * ny];
+                        // bilinear_replicate (dis_device.h), split at the loads
+                        X[m] = clamp_m1((float)x + v[m].x, (float)cW);
+                        Y[m] = clamp_m1((float)y + v[m].y, (float)a.c_H);
+                        const int xa = (int)floorf(X[m]), ya = (int)floorf(Y[m]);
+                        const int c0 = clampi(xa, 0, cW - 1), c1 = clampi(xa + 1, 0, cW - 1);
+                        const unsigned o0 = __umul24((unsigned)clampi(ya, 0, a.c_H - 1), (unsigned)cW);
+                        const unsigned o1 = __umul24((unsigned)clampi(ya + 1, 0, a.c_H - 1), (unsigned)cW);
+                        tp[m][0] = I1c[o0 + c0];
+                        tp[m][1] = I1c[o0 + c1];
+                        tp[m][2] = I1c[o1 + c0];
+                        tp[m][3] = I1c[o1 + c1];
                     }
-                    fx = fx + quad_perm<kQuadEven>(cvx);
-                    fy = fy + quad_perm<kQuadEven>(cvy);
-                    wt = wt + quad_perm<kQuadEven>(c);
-                    if (2 * m + 1 < n) {
-                        fx = fx + quad_perm<kQuadOdd>(cvx);
-                        fy = fy + quad_perm<kQuadOdd>(cvy);
-                        wt = wt + quad_perm<kQuadOdd>(c);
+#pragma unroll
+                    for (int m = 0; m < kPV; ++m) {
+                        if (2 * m >= n) break;
+                        const float fx0 = floorf(X[m]), fy0 = floorf(Y[m]);
+                        const float ax = X[m] - fx0, ay = Y[m] - fy0;
+                        const float top = (1.0f - ax) * tp[m][0] + ax * tp[m][1];
+                        const float bot = (1.0f - ax) * tp[m][2] + ax * tp[m][3];
+                        const float d = ((1.0f - ay) * top + ay * bot) - i0v;
+                        const float c = recip_max1(d);  // correctly rounded (dis_device.h)
+                        const bool own = 2 * m + q < n;
+                        const float cvx = own ? c * v[m].x : 0.0f, cvy = own ? c * v[m].y : 0.0f;
+                        const float cw = own ? c : 0.0f;
+                        fx = fx + quad_perm<kQuadEven>(cvx);
+                        fy = fy + quad_perm<kQuadEven>(cvy);
+                        wt = wt + quad_perm<kQuadEven>(cw);
+                        if (2 * m + 1 < n) {
+                            fx = fx + quad_perm<kQuadOdd>(cvx);
+                            fy = fy + quad_perm<kQuadOdd>(cvy);
+                            wt = wt + quad_perm<kQuadOdd>(cw);
+                        }
+                    }
+                } else {
+                    for (int m = 0; 2 * m < n; ++m) {
+                        const int t = 2 * m + q;
+                        float c = 0.0f, cvx = 0.0f, cvy = 0.0f;
+                        if (t < n) {
+                            const int i = floordiv_r(t, rny);
+                            const float2 v = cu[(xr.x + i) * PH + yr.x + t - i * ny];
+                            const float d = bilinear_replicate(I1c, cW, a.c_H, (float)x + v.x, (float)y + v.y) - i0v;
+                            c = recip_max1(d);  // correctly rounded (dis_device.h)
+                            cvx = c * v.x;
+                            cvy = c * v.y;
+                        }
+                        fx = fx + quad_perm<kQuadEven>(cvx);
+                        fy = fy + quad_perm<kQuadEven>(cvy);
+                        wt = wt + quad_perm<kQuadEven>(c);
+                        if (2 * m + 1 < n) {
+                            fx = fx + quad_perm<kQuadOdd>(cvx);
+                            fy = fy + quad_perm<kQuadOdd>(cvy);
+                            wt = wt + quad_perm<kQuadOdd>(c);
+                        }
                     }
                 }
             } else {
