@@ -406,11 +406,12 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 // fixed row stride (a vote's lower taps at constant LDS offsets). F >= 1:
 // 48 x 50 keeps the workgroup at 23 KB of LDS, 7 per CU (56 x 56: 26 KB, 6 per
 // CU, measured 6 % slower); a window whose flows spread wider than ~11 level-F
-// pixels reads I1 globally instead (same values)
+// pixels reads I1 globally instead (same values); F == 0: 80 x 80 (the box
+// is at least 67 x 67)
 template <bool UPS>
 constexpr int kPaperStage = UPS ? 48 * 50 : 80 * 80;
 template <bool UPS>
-constexpr int kPaperSS = UPS ? 48 : 96;
+constexpr int kPaperSS = UPS ? 48 : 80;
 
 // one float4 (two output pixels) of the flow. (Streaming, non-temporal
 // stores made the one-stream kernel trace faster -- the next call's pyramid
