@@ -547,21 +547,21 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         // I0 of the window, parked in the .x of each pixel's dense slot (the
         // pixel's densify reads it there before writing the slot), the loads
         // issued together with the patch staging's
-        constexpr int NW = (kOutSW * kOutSH + 255) / 256;
+        // (lane = column, wave + 4 j = row: no index division; lanes and rows
+        // past the window reload its last column / row and store nothing)
         const float* I0 = a.img0 + (size_t)pair * a.plane_stride;
-        const float rrw0 = __builtin_amdgcn_rcpf((float)rw);
-        float v0[NW];
+        constexpr int NR = (kOutSH + 3) / 4;
+        const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            const int k = tid + 256 * j;
-            const int r = floordiv_r(k, rrw0), c = k - r * rw;
-            v0[j] = k < rw * rh ? I0[(size_t)(j0 + r) * a.wF + i0 + c] : 0.0f;
-        }
+        for (int cb = 0; cb < kOutSW; cb += 64) {
+            const int c = cb + lane;
+            const float* col = I0 + (size_t)j0 * a.wF + i0 + min(c, rw - 1);
+            float v0[NR];
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            const int k = tid + 256 * j;
-            const int r = floordiv_r(k, rrw0), c = k - r * rw;
-            if (k < rw * rh) dense[r * kOutSW + c].x = v0[j];
+            for (int j = 0; j < NR; ++j) v0[j] = col[(size_t)min(wv + 4 * j, rh - 1) * a.wF];
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+                if (wv + 4 * j < rh && c < rw) dense[(wv + 4 * j) * kOutSW + c].x = v0[j];
         }
     }
     if (!kPaper && tid >= 64 && tid - 64 <= K * K) {
@@ -665,23 +665,22 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const int shs = by1 - by0 + 1;
             staged = sws > 0 && shs > 0 && sws <= kPaperSS<UPSAMPLE> && shs * kPaperSS<UPSAMPLE> <= kPaperStage<UPSAMPLE>;
             if (staged) {  // every load issued before the first store: one memory latency
-                constexpr int NS = (kPaperStage<UPSAMPLE> + 255) / 256;
+                // lane = column, wave + 4 j = row (as the I0 window above)
+                constexpr int SS = kPaperSS<UPSAMPLE>, NR = (kPaperStage<UPSAMPLE> / SS + 3) / 4;
                 const float* I1 = a.img1 + (size_t)pair * a.plane_stride;
-                const float rsw = __builtin_amdgcn_rcpf((float)sws);
-                const int n1 = sws * shs;
-                float v1[NS];
-                int at[NS];
+                const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    const int k = tid + 256 * j;
-                    const int r = floordiv_r(k, rsw), c = k - r * sws;
-                    at[j] = r * kPaperSS<UPSAMPLE> + c;
-                    v1[j] = k < n1 ? I1[(size_t)clampi(by0 + r, 0, a.hF - 1) * a.wF + clampi(bx0 + c, 0, a.wF - 1)]
-                                   : 0.0f;
+                for (int cb = 0; cb < SS; cb += 64) {
+                    const int c = cb + lane;
+                    const float* col = I1 + clampi(bx0 + min(c, sws - 1), 0, a.wF - 1);
+                    float v1[NR];
+#pragma unroll
+                    for (int j = 0; j < NR; ++j)
+                        v1[j] = col[(size_t)clampi(by0 + min(wv + 4 * j, shs - 1), 0, a.hF - 1) * a.wF];
+#pragma unroll
+                    for (int j = 0; j < NR; ++j)
+                        if (wv + 4 * j < shs && c < sws) s1[(wv + 4 * j) * SS + c] = v1[j];
                 }
-#pragma unroll
-                for (int j = 0; j < NS; ++j)
-                    if (tid + 256 * j < n1) s1[at[j]] = v1[j];
             }
         }
         __syncthreads();
