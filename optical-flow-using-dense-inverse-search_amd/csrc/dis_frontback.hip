@@ -361,24 +361,29 @@ hipError_t launch_pyramid(const PyramidArgs& a, int batch, hipStream_t s, Timing
 namespace {
 
 // full-resolution output tile per workgroup (measured: 64 rows beat 16 by
-// 2.3 % of the step at F >= 1)
+// 2.3 % of the step at F >= 1); at F == 0 32 rows: the level-0 window halves
+// the LDS (paper mode 70 -> 39 KB, 2 -> 4 workgroups per CU, -6 % per SLOW
+// step; reference mode 44 -> 24 KB, -1 %). Paper mode at F >= 1 with 32 rows
+// measured 2 % slower (7 -> 8 workgroups per CU do not pay for the halo).
 constexpr int kOutTW = 64, kOutTH = 64;
+template <bool UPS>
+constexpr int kOutTHf = UPS ? kOutTH : 32;  // rows of an output tile
 
 // LDS shapes per instantiation: level-F window (F == 0 is the widest; F >= 1
 // needs half the tile + the interpolation halo) and the staged patch block for
 // K = ceil(ps/steps) covering patches per axis (steps >= ceil(8/K), ps = 8).
-template <bool UPS>
+template <bool UPS, int TH>
 struct OutShape {
     static constexpr int SW = UPS ? kOutTW / 2 + 3 : kOutTW + 3;
-    static constexpr int SH = UPS ? kOutTH / 2 + 3 : kOutTH + 3;
+    static constexpr int SH = UPS ? TH / 2 + 3 : TH + 3;
 };
-template <bool UPS, int K>
+template <bool UPS, int K, int TH>
 struct OutPatch {
     static constexpr int st = (8 + K - 1) / K;
-    static constexpr int PX = (OutShape<UPS>::SW + 7) / st + 2;
+    static constexpr int PX = (OutShape<UPS, TH>::SW + 7) / st + 2;
     // odd stride (in float2): the densify's lanes read patches at different
     // column offsets xr.x, which an even stride maps onto the same LDS banks
-    static constexpr int PY = ((OutShape<UPS>::SH + 7) / st + 2) | 1;
+    static constexpr int PY = ((OutShape<UPS, TH>::SH + 7) / st + 2) | 1;
 };
 
 // cv::resize INTER_LINEAR source index / fraction for destination index d at
@@ -406,10 +411,10 @@ __device__ __forceinline__ void lin_coef(int d, int n_src, int F, int* i, float*
 // fixed row stride (a vote's lower taps at constant LDS offsets). F >= 1:
 // 48 x 50 keeps the workgroup at 23 KB of LDS, 7 per CU (56 x 56: 26 KB, 6 per
 // CU, measured 6 % slower); a window whose flows spread wider than ~11 level-F
-// pixels reads I1 globally instead (same values); F == 0: 80 x 80 (the box
-// is at least 67 x 67)
+// pixels reads I1 globally instead (same values); F == 0 (32-row tiles):
+// 80 x 48 (the box is at least 67 x 35)
 template <bool UPS>
-constexpr int kPaperStage = UPS ? 48 * 50 : 80 * 80;
+constexpr int kPaperStage = UPS ? 48 * 50 : 80 * 48;
 template <bool UPS>
 constexpr int kPaperSS = UPS ? 48 : 80;
 
@@ -475,8 +480,9 @@ __device__ __forceinline__ void out_rows_f1(const OutputArgs& a, const float2* d
 template <bool UPSAMPLE, int K, bool kPaper = false>
 __global__ void __launch_bounds__(256) k_output(OutputArgs a)
 {
-    constexpr int kOutSW = OutShape<UPSAMPLE>::SW, kOutSH = OutShape<UPSAMPLE>::SH;
-    constexpr int kOutPX = OutPatch<UPSAMPLE, K>::PX, kOutPY = OutPatch<UPSAMPLE, K>::PY;
+    constexpr int kTH = kOutTHf<UPSAMPLE>;
+    constexpr int kOutSW = OutShape<UPSAMPLE, kTH>::SW, kOutSH = OutShape<UPSAMPLE, kTH>::SH;
+    constexpr int kOutPX = OutPatch<UPSAMPLE, K, kTH>::PX, kOutPY = OutPatch<UPSAMPLE, K, kTH>::PY;
     __shared__ float2 pu[(kOutPX + K + 2) * kOutPY];  // + the padding the unmasked taps may read
     __shared__ float rtab[K * K + 1];                  // RN(1 / (0.5 n)), n covering patches
     __shared__ float2 dense[kOutSW * kOutSH];
@@ -489,7 +495,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     __shared__ unsigned char csort[kPaper ? kOutSW : 1], rsort[kPaper ? kOutSH : 1];
     __shared__ int4 ctab[K + 1];
     const int tid = threadIdx.x;
-    const int ox = blockIdx.x * kOutTW, oy = blockIdx.y * kOutTH;
+    const int ox = blockIdx.x * kOutTW, oy = blockIdx.y * kTH;
     const int pair = blockIdx.z;
     const float2* u = a.u + (size_t)pair * a.u_stride;
     if (kPaper && tid == 0) {
@@ -504,14 +510,14 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         lin_coef(ox + a.pad_left, a.wF, a.F, &i0, &f);
         lin_coef(min(ox + kOutTW - 1, a.W - 1) + a.pad_left, a.wF, a.F, &i1, &f);
         lin_coef(oy + a.pad_top, a.hF, a.F, &j0, &f);
-        lin_coef(min(oy + kOutTH - 1, a.H - 1) + a.pad_top, a.hF, a.F, &j1, &f);
+        lin_coef(min(oy + kTH - 1, a.H - 1) + a.pad_top, a.hF, a.F, &j1, &f);
         i1 = min(i1 + 1, a.wF - 1);
         j1 = min(j1 + 1, a.hF - 1);
     } else {
         i0 = ox + a.pad_left;
         j0 = oy + a.pad_top;
         i1 = min(ox + kOutTW - 1, a.W - 1) + a.pad_left;
-        j1 = min(oy + kOutTH - 1, a.H - 1) + a.pad_top;
+        j1 = min(oy + kTH - 1, a.H - 1) + a.pad_top;
     }
     const int rw = i1 - i0 + 1, rh = j1 - j0 + 1;
     // patches whose footprint meets the window
@@ -791,11 +797,11 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         densify(std::false_type{});
     __syncthreads();
 
-    constexpr int RPT = kOutTH / 8;  // output rows per thread
+    constexpr int RPT = kTH / 8;  // output rows per thread
     const int px = ox + (tid & 31) * 2, py = oy + (tid >> 5) * RPT;
     if constexpr (UPSAMPLE) {
-        const int xh = ox + kOutTW - 1 + a.pad_left, yh = oy + kOutTH - 1 + a.pad_top;
-        if (a.F == 1 && a.vec_store && ox + kOutTW <= a.W && oy + kOutTH <= a.H && ox + a.pad_left >= 1 &&
+        const int xh = ox + kOutTW - 1 + a.pad_left, yh = oy + kTH - 1 + a.pad_top;
+        if (a.F == 1 && a.vec_store && ox + kOutTW <= a.W && oy + kTH <= a.H && ox + a.pad_left >= 1 &&
             oy + a.pad_top >= 1 && ((xh - 1) >> 1) + 1 <= a.wF - 1 && ((yh - 1) >> 1) + 1 <= a.hF - 1 &&
             xh < a.xmax) {  // uniform: an interior tile
             switch (((a.pad_top - 1) & 1) * 2 + ((a.pad_left - 1) & 1)) {
@@ -886,7 +892,8 @@ static void launch_output_k(const OutputArgs& a, dim3 grid, hipStream_t s, Timin
 hipError_t launch_output(const OutputArgs& a, int batch, hipStream_t s, Timing t)
 {
     if (!output_fits(a)) return hipErrorInvalidValue;
-    dim3 grid((a.W + kOutTW - 1) / kOutTW, (a.H + kOutTH - 1) / kOutTH, batch);
+    const int th = a.F == 0 ? kOutTHf<false> : kOutTHf<true>;
+    dim3 grid((a.W + kOutTW - 1) / kOutTW, (a.H + th - 1) / th, batch);
     switch ((2 * a.hp + a.steps - 1) / a.steps) {  // K = ceil(ps / steps)
         case 1: launch_output_k<1>(a, grid, s, t); break;
         case 2: launch_output_k<2>(a, grid, s, t); break;
