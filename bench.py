@@ -127,11 +127,14 @@ def _cpu_worker(args):
 
     params = disflow.Params(**pfields)
     I0s, I1s = _CPU_POOL
-    n, k = 0, k0
+    # worker w takes pairs w, w + step, w + 2 step, ... of the global sequence
+    # and cycles the pool by its own count (k0 + n*step modulo a
+    # pool of `step` pairs would revisit one pair forever)
+    n = 0
     while True:
-        oracle_binding.calc_from_params(I0s[k % len(I0s)], I1s[k % len(I1s)], params)
+        k = (k0 + n) % len(I0s)
+        oracle_binding.calc_from_params(I0s[k], I1s[k], params)
         n += 1
-        k += step
         if time.time() >= deadline:
             return n
 
@@ -156,8 +159,14 @@ def cpu_baseline(params, W, H, budget_s, workers):
         ctx = mp.get_context("fork")
         t0 = time.time()
         deadline = t0 + 2 * budget_s / 3
-        with ctx.Pool(workers) as pool:
+        # close + join (not the context manager, whose exit terminate()s the
+        # workers: under rocprofv3 that SIGTERM printed an abort trace)
+        pool = ctx.Pool(workers)
+        try:
             ns = pool.map(_cpu_worker, [(w, workers, pf, deadline) for w in range(workers)])
+        finally:
+            pool.close()
+            pool.join()
         out.update(value=sum(ns) / (time.time() - t0), cores=workers, pairs=sum(ns))
     else:
         out.update(value=n1 / t1, cores=1, pairs=n1)

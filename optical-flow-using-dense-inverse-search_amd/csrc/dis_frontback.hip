@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     __shared__ float2 dense[kOutSW * kOutSH];
     __shared__ int2 cr[kOutSW], rr[kOutSH];
     __shared__ float s1[kPaper ? kPaperStage<UPSAMPLE> : 1];  // paper mode: staged I1 (see below)
-    __shared__ int pbox[4];
+    __shared__ int pbox[5];
     // paper mode: window columns / rows sorted by their covering-patch count,
     // and per column class v (count v): first pixel index, first sorted
     // column, columns, RCP(columns) bits (see the densify loop)
@@ -501,6 +501,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     if (kPaper && tid == 0) {
         pbox[0] = pbox[1] = 0x7fffffff;
         pbox[2] = pbox[3] = -0x7fffffff;
+        pbox[4] = 0;
     }
 
     // level-F window of this tile
@@ -527,6 +528,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
     const int ha = max(0, floordiv_r(j0 - a.offh - hp + st, rst)), hb = min(a.nph - 1, floordiv_r(j1 - a.offh + hp, rst));
     const int PW = gb - ga + 1, PH = hb - ha + 1;  // <= kOutPX x kOutPY (output_fits)
     float umin_x = INFINITY, umin_y = INFINITY, umax_x = -INFINITY, umax_y = -INFINITY;  // paper mode
+    bool u_nan = false;  // paper mode: a staged patch with a NaN displacement (see the I1 box below)
     {
         constexpr int NL = (kOutPX * kOutPY + 255) / 256;
         float2 v[NL];
@@ -541,6 +543,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
                 umax_x = fmaxf(umax_x, v[j].x);
                 umin_y = fminf(umin_y, v[j].y);
                 umax_y = fmaxf(umax_y, v[j].y);
+                u_nan |= v[j].x != v[j].x || v[j].y != v[j].y;
             }
         }
         // new_u = u * 0.5 (src/patch_grid.cpp:156), formed once per patch (paper mode: u itself)
@@ -649,6 +652,12 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
         auto fl = [](float v) { return (int)fminf(fmaxf(floorf(v), -1048576.0f), 1048576.0f); };
         int m0 = umin_x <= umax_x ? fl(umin_x) : 0x7fffffff, m1 = umin_y <= umax_y ? fl(umin_y) : 0x7fffffff;
         int m2 = umin_x <= umax_x ? fl(umax_x) : -0x7fffffff, m3 = umin_y <= umax_y ? fl(umax_y) : -0x7fffffff;
+        // The staged taps' LDS index comes from v_med3 clamps, which do not
+        // clamp NaN, and fminf / fmaxf above skip NaN. The search never leaves
+        // a NaN displacement (it resets them like outliers), but should one
+        // reach this kernel, the whole tile takes the global (replicate-
+        // clamped) reads instead of the stage (pbox[4]).
+        const bool wave_nan = __ballot(u_nan) != 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             m0 = min(m0, __shfl_xor(m0, o));
@@ -657,6 +666,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             m3 = max(m3, __shfl_xor(m3, o));
         }
         if ((tid & 63) == 0) {
+            if (wave_nan) pbox[4] = 1;
             atomicMin(&pbox[0], m0);
             atomicMin(&pbox[1], m1);
             atomicMax(&pbox[2], m2);
@@ -669,7 +679,7 @@ __global__ void __launch_bounds__(256) k_output(OutputArgs a)
             const int bx1 = min(i1 + pbox[2] + 1, a.wF) + 1, by1 = min(j1 + pbox[3] + 1, a.hF) + 1;
             sws = bx1 - bx0 + 1;
             const int shs = by1 - by0 + 1;
-            staged = sws > 0 && shs > 0 && sws <= kPaperSS<UPSAMPLE> && shs * kPaperSS<UPSAMPLE> <= kPaperStage<UPSAMPLE>;
+            staged = !pbox[4] && sws > 0 && shs > 0 && sws <= kPaperSS<UPSAMPLE> && shs * kPaperSS<UPSAMPLE> <= kPaperStage<UPSAMPLE>;
             if (staged) {  // every load issued before the first store: one memory latency
                 // lane = column, wave + 4 j = row (as the I0 window above)
                 constexpr int SS = kPaperSS<UPSAMPLE>, NR = (kPaperStage<UPSAMPLE> / SS + 3) / 4;
