@@ -352,6 +352,11 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # read-only sclk / socket-power samples of this rank's GPU (amdgpu hwmon)
+    # during the timed region and the roofline pass: a VALU-bound kernel's time
+    # follows the clock, which follows the power cap
+    from disflow import boxstate
+    sampler = boxstate.Sampler(boxstate.torch_hwmon_dir(local))
     if world > 1:
         import torch.distributed as dist
         if a.dist_backend == "nccl":
@@ -398,12 +403,13 @@ def main():
 
     barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    el = time.perf_counter() - t0
+    with sampler.phase("timed"):
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        barrier()
+        el = time.perf_counter() - t0
 
     # roofline pass (after the timed region): the same steps with the batch on
     # one stream, so the finest-level search launch runs without co-running
@@ -413,9 +419,10 @@ def main():
         eng.set_concurrency(1)
         step()
         eng.set_kernel_timing(True)  # (re)enabling starts a fresh measurement
-        for _ in range(max(10, a.steps // 5)):
-            step()
-        torch.cuda.synchronize(dev)
+        with sampler.phase("roofline"):
+            for _ in range(max(10, a.steps // 5)):
+                step()
+            torch.cuda.synchronize(dev)
         n_f, ms_f = eng.kernel_time(disflow.KERNEL_SEARCH_FINEST)
         eng.set_kernel_timing(False)
         eng.set_concurrency(a.streams if a.streams else 2)
@@ -582,6 +589,11 @@ def main():
         except Exception:
             traffic = None
 
+    sampler.close()
+    box = {"hwmon": sampler.dir, "timed": sampler.summary("timed"), "roofline_pass": sampler.summary("roofline"),
+           "note": "rank 0's GPU: sclk (hwmon freq1_input) and socket power (power1_input) sampled every ~2 ms, "
+                   "read-only; the quoted peaks assume 2400 MHz"}
+    clock = (box["roofline_pass"] or {}).get("sclk_MHz_mean")
     if rank == 0:
         pairs = world * B * a.steps
         line = {
@@ -609,6 +621,9 @@ def main():
                          "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / VALU_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
                          "avg_launch_ms": avg_ms, "launches": n_f,
+                         "clock_MHz": clock,
+                         "frac_at_clock": (achieved / (VALU_PEAK_TFLOPS * clock / 2400.0))
+                         if (achieved and clock) else None,
                          "algorithmic_flops_per_launch": flops_per_launch,
                          "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": (achieved_gbs / HBM_PEAK_GBS) if achieved_gbs else None,
@@ -617,9 +632,11 @@ def main():
                                  "FLOPs = DESIGN.md 4 count x patches in the launch (all B pairs); "
                                  "duration = HIP dispatch events of the finest-level launch in a "
                                  "one-stream pass after the timed region; traffic = PMC HBM bytes per "
-                                 "launch of that kernel (profiles/traffic.json)"},
+                                 "launch of that kernel (profiles/traffic.json); clock_MHz = mean sclk sampled "
+                                 "during that pass, frac_at_clock = achieved / (peak x clock / 2400 MHz)"},
             "pipeline_hbm_frac": wl["algorithmic_bytes"] * pairs / el / 1e9 / HBM_PEAK_GBS,
             "hbm_measured_peak": hbm_meas,
+            "box_state": box,
             "cpu_baseline": cpu,
             "gather": gather,
             "max_epe_vs_oracle": max_epe,

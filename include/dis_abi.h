@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DIS_ABI_VERSION 7
+#define DIS_ABI_VERSION 8
 
 typedef enum dis_status {
     DIS_OK = 0,
@@ -121,6 +121,27 @@ dis_status dis_calc_batch_u8(dis_ctx* ctx, int n, const uint8_t* I0, const uint8
                              size_t stride, size_t pair_stride, float* flow,
                              dis_mem where, void* stream);
 
+/* Host-frame path (ABI v8): with DIS_MEM_HOST a batch runs in chunks of
+ * chunk_pairs pairs (0 = auto, the default: about 64 MB of flow per chunk)
+ * through two device slots; chunk j+1's upload, chunk j's computation and
+ * chunk j-1's download overlap (the downloads are issued by a thread of the
+ * context). The copies go straight between the caller's buffers and the
+ * device; page-locked caller buffers (dis_host_alloc, hipHostMalloc /
+ * hipHostRegister) make them asynchronous. The results are the device path's,
+ * bit for bit, for any chunking. The reference's per-pair loop hands over host
+ * frames and gets host flow back (src/main.cpp:102-206). */
+dis_status dis_set_host_pipeline(dis_ctx* ctx, int chunk_pairs);
+typedef struct dis_host_info {
+    int chunk_pairs;     /* pairs per chunk (0 before the first host call)          */
+    int last_chunks;     /* chunks of the last host call                            */
+    int last_direct_in;  /* 1: the last host call's frames were page-locked         */
+    int last_direct_out; /* 1: the last host call's flow buffer was page-locked     */
+} dis_host_info;
+dis_status dis_host_pipeline_info(dis_ctx* ctx, dis_host_info* out);
+/* Page-locked host memory for frames and flows (hipHostMalloc); no context. */
+dis_status dis_host_alloc(size_t bytes, void** out);
+dis_status dis_host_free(void* p);
+
 /* Compatibility entry with the exact semantics of the reference constructor
  * OpticalFlowClass(...) (include/optical_flow.hpp:43-54): host pyramids of
  * (coarsest+1) PADDED planes (row stride W_l + 2*img_padding, pointer at the
@@ -198,6 +219,19 @@ dis_status dis_set_kernel_variant(dis_ctx* ctx, int variant);
  * the legacy default stream meanwhile, HIP invalidates it and that call runs
  * eagerly instead. Results do not depend on this setting. */
 dis_status dis_set_graphs(dis_ctx* ctx, int enable);
+
+/* Stream plans of a batch call (ABI v8; host only, no device needed). Ops are
+ * 4 ints each: {kind (0 record, 1 wait, 2 work), stream (0 = the caller's,
+ * 1 + k = sub-batch stream k), event (0 = fork, 1 + k = sub-batch k's join),
+ * stage}. dis_batch_stream_plan writes the plan a call with `nsub` (2..8)
+ * sub-batches and `nstages` stages issues (count ops; ops may be NULL to ask
+ * for the count). dis_check_stream_plan applies the rules a plan must keep to
+ * be captured into a HIP graph (every waited event recorded in the capture,
+ * work only on streams in it, every stream joined back) and
+ * returns DIS_ERR_UNSUPPORTED with the broken rule in dis_last_error()
+ * otherwise. The runtime checks its plan this way before every capture. */
+dis_status dis_batch_stream_plan(int nsub, int nstages, int* ops, int capacity, int* count);
+dis_status dis_check_stream_plan(const int* ops, int nops, int nstreams, int nevents);
 
 typedef enum dis_precision { DIS_PRECISION_EXACT = 0, DIS_PRECISION_FMA = 1 } dis_precision;
 dis_status dis_set_precision(dis_ctx* ctx, int mode);

@@ -6,19 +6,25 @@
 // crop) around src/optical_flow.cpp:67-91 (coarse-to-fine scale loop).
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
 
 #include "dis_kernels.h"
+#include "dis_plan.h"
 
 namespace {
+
 
 thread_local std::string g_err;
 
@@ -120,6 +126,105 @@ static int search8_lanes(int variant, long long patches, int steps)
 // per sub-batch: the levels' fallback list counts (k_search8_fb)
 constexpr size_t kFbCounters = dis::kMaxLevels;
 
+// Host-frame path state (dis_calc_batch_u8 with DIS_MEM_HOST), made on the
+// first host call: the batch runs in chunks of `chunk` pairs through two
+// device staging slots, so that the upload of chunk j+1, the computation of
+// chunk j and the download of chunk j-1 overlap (the reference's own pattern
+// is host frames in, host flow out per pair, src/main.cpp:115-116,184-189).
+// The copies go straight between the caller's buffers and the device: a
+// hipMemcpyAsync on pageable memory runs at the DMA rate but returns only when
+// it is done (tools/host_xfer_probe.hip), so the downloads are issued by a
+// thread of their own while the calling thread uploads and enqueues. Staging
+// through page-locked buffers with threaded host copies, and host waits
+// instead of stream waits in front of the copies, measured slower (DESIGN.md
+// 4, host-frame path).
+struct HostPipe {
+    int chunk = 0;
+    size_t frame = 0;                 // bytes of one frame (W * H)
+    uint8_t* din[2] = {};             // device: chunk I0 frames, then chunk I1 frames
+    float2* dout[2] = {};             // device: chunk flows
+    hipStream_t up = nullptr, down = nullptr;
+    hipEvent_t up_done[2] = {}, comp_done[2] = {}, down_done[2] = {};
+    bool comp_pending[2] = {}, down_pending[2] = {};
+    // the download thread: jobs in chunk order; `issued` counts the jobs whose
+    // copy has been issued and whose down_done event has been recorded
+    struct Job {
+        char* dst;
+        const char* src;
+        size_t bytes;
+        int slot;
+    };
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<Job> q;
+    long long posted = 0, issued = 0;
+    hipError_t err = hipSuccess;
+    bool stop = false;
+    int device = 0;
+    // what the last host call did (dis_host_pipeline_info)
+    int last_chunks = 0, last_direct_in = 0, last_direct_out = 0;
+
+    void run()
+    {
+        (void)hipSetDevice(device);
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                j = q.front();
+                q.erase(q.begin());
+            }
+            hipError_t e = hipStreamWaitEvent(down, comp_done[j.slot], 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost, down);
+            if (e == hipSuccess) e = hipEventRecord(down_done[j.slot], down);
+            std::lock_guard<std::mutex> l(mu);
+            if (e != hipSuccess && err == hipSuccess) err = e;
+            ++issued;
+            done_cv.notify_all();
+        }
+    }
+    void post(const Job& j)
+    {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            q.push_back(j);
+            ++posted;
+        }
+        cv.notify_one();
+    }
+    // wait until the first `k` posted jobs are issued; the first error seen
+    hipError_t wait_issued(long long k)
+    {
+        std::unique_lock<std::mutex> l(mu);
+        done_cv.wait(l, [&] { return issued >= k; });
+        const hipError_t e = err;
+        err = hipSuccess;
+        return e;
+    }
+    ~HostPipe()
+    {
+        if (th.joinable()) {
+            {
+                std::lock_guard<std::mutex> l(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            th.join();
+        }
+        for (int s = 0; s < 2; ++s) {
+            hipFree(din[s]);
+            hipFree(dout[s]);
+            for (hipEvent_t e : {up_done[s], comp_done[s], down_done[s]})
+                if (e) hipEventDestroy(e);
+        }
+        if (up) hipStreamDestroy(up);
+        if (down) hipStreamDestroy(down);
+    }
+};
+
 struct dis_ctx {
     dis_params p;
     dis::Geometry g;
@@ -191,9 +296,11 @@ struct dis_ctx {
     // fb + fb_list_off[k][level]
     int* fb = nullptr;
     size_t fb_list_off[8][dis::kMaxLevels] = {};
-    uint8_t* in0 = nullptr;  // host-mode input staging
-    uint8_t* in1 = nullptr;
-    float2* out = nullptr;   // host-mode output staging
+    // host-frame path (DIS_MEM_HOST): device slots, streams and the download
+    // thread made on the first host call; dis_set_host_pipeline sets the chunk
+    // (0 = auto)
+    std::unique_ptr<HostPipe> hp;
+    int host_chunk = 0;
     // kernel timing
     int timing = 0;
     struct Rec {
@@ -248,12 +355,9 @@ void free_ws(dis_ctx* c)
     c->fb = nullptr;
     hipFree(c->vr_ws);
     c->vr_ws = nullptr;
-    hipFree(c->in0);
-    hipFree(c->in1);
-    hipFree(c->out);
+    c->hp.reset();
     c->img0 = c->img1 = c->dx = c->dy = nullptr;
-    c->pu = c->dense = c->out = nullptr;
-    c->in0 = c->in1 = nullptr;
+    c->pu = c->dense = nullptr;
 }
 
 // Per-launch timing: when enabled, hands out an event pair from the pool to be
@@ -684,20 +788,40 @@ dis_status run_batches(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, 
     // with sub[1] -- serialising the two sub-batches -- depended on how many
     // streams the process had created before: 15k vs 20k pairs/s at 1080p.
     // The context's own streams are created back to back, on distinct queues.)
-    DIS_HIP(hipEventRecord(c->fork, s));
-    for (int k = 0; k < S; ++k) DIS_HIP(hipStreamWaitEvent(c->sub[k], c->fork, 0));
-    const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
-    for (size_t i = 0; i < stages.size() * S; ++i) {  // stage-major
-        const int k = (int)(i % S), st = stages[i / S];
-        const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
-        StageRange range(st, k);
-        dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
-                                 stride, pair_stride, flow + (size_t)a * fpp, c->sub[k], st);
-        if (r != DIS_OK) return r;
+    // The fork / stages / join sequence as a plan (dis_plan.h): checked against
+    // the capture rules before a capture issues any of it -- a plan the HIP
+    // runtime cannot capture (an unjoined stream) fails at EndCapture and
+    // leaves a stream in capture mode and an invalid graph handle behind
+    // (tools/capture_probe.hip) -- then executed op by op.
+    const std::vector<dis::PlanOp> plan = dis::batch_plan(S, (int)stages.size());
+    if (capturing) {
+        const std::string why = dis::check_capture_plan(plan.data(), (int)plan.size(), 1 + S, 1 + S);
+        if (!why.empty()) return fail(DIS_ERR_INTERNAL, "batch stream plan cannot be captured: " + why);
     }
-    for (int k = 0; k < S; ++k) {
-        DIS_HIP(hipEventRecord(c->join[k], c->sub[k]));
-        DIS_HIP(hipStreamWaitEvent(s, c->join[k], 0));
+    auto stream_of = [&](int x) { return x == 0 ? s : c->sub[x - 1]; };
+    auto event_of = [&](int e) { return e == 0 ? c->fork : c->join[e - 1]; };
+    const size_t fpp = (size_t)c->g.W * c->g.H;  // float2 per output pair
+    for (const dis::PlanOp& o : plan) {
+        if (o.kind == dis::kOpRecord) {
+            DIS_HIP(hipEventRecord(event_of(o.event), stream_of(o.stream)));
+        } else if (o.kind == dis::kOpWait) {
+            DIS_HIP(hipStreamWaitEvent(stream_of(o.stream), event_of(o.event), 0));
+            if (capturing) {  // the waiting stream must now be in the origin's capture
+                hipStreamCaptureStatus cs0, cs1;
+                unsigned long long id0 = 0, id1 = 0;
+                DIS_HIP(hipStreamGetCaptureInfo(s, &cs0, &id0));
+                DIS_HIP(hipStreamGetCaptureInfo(stream_of(o.stream), &cs1, &id1));
+                if (cs0 != hipStreamCaptureStatusActive || cs1 != hipStreamCaptureStatusActive || id0 != id1)
+                    return fail(DIS_ERR_DEVICE, "graph capture: a sub-batch stream did not join the call's capture");
+            }
+        } else {
+            const int k = o.stream - 1, st = stages[o.stage];
+            const int a = (int)((long long)n * k / S), b = (int)((long long)n * (k + 1) / S);
+            StageRange range(st, k);
+            dis_status r = run_batch(c, k, b - a, a, I0 + (size_t)a * pair_stride, I1 + (size_t)a * pair_stride,
+                                     stride, pair_stride, flow + (size_t)a * fpp, stream_of(o.stream), st);
+            if (r != DIS_OK) return r;
+        }
     }
     c->last_batch = n;
     if (capturing) return DIS_OK;
@@ -753,6 +877,21 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
             e0 = hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal);
             r = e0 == hipSuccess ? run_batches(c, n, I0, I1, stride, pair_stride, flow, c->cap, true) : DIS_OK;
             e = e0 == hipSuccess ? hipStreamEndCapture(c->cap, &graph) : e0;
+            // HIP 7.2: a failed EndCapture writes a non-null handle that is not a
+            // graph (instantiating it crashed tools/capture_probe, destroying it
+            // returns hipErrorIllegalState) -- never touch it
+            if (e != hipSuccess) graph = nullptr;
+            // and a stream it left unjoined stays in capture mode (mode 5): no
+            // later work may go to the pooled streams then
+            for (int k = 0; k < dis_ctx::kMaxSub; ++k) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(c->sub[k], &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+                    (void)hipGetLastError();
+                    c->graphs = 0;
+                    return fail(DIS_ERR_DEVICE, "graph capture left sub-batch stream " + std::to_string(k) +
+                                                    " in capture mode (" + hipGetErrorName(e) + ")");
+                }
+            }
         }
         hipError_t e2 = hipErrorUnknown;
         if (r == DIS_OK && e == hipSuccess) {
@@ -818,6 +957,143 @@ dis_status run_batches_graph(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
     return DIS_OK;
 }
 
+// True when [p, p + bytes) lies in one page-locked host allocation
+// (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory): the DMA engines
+// read or write it directly, no staging copy.
+bool host_pinned(const void* p, size_t bytes)
+{
+    if (!p || !bytes) return false;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error here
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+    void *b0 = nullptr, *b1 = nullptr;
+    const char* last = static_cast<const char*>(p) + bytes - 1;
+    if (hipPointerGetAttribute(&b0, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<void*>(p)) != hipSuccess ||
+        hipPointerGetAttribute(&b1, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<char*>(last)) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return b0 && b0 == b1;
+}
+
+// Device slots, streams and the download thread of the host-frame path, made
+// on the first host call (device-resident callers never pay for them).
+// chunk = 0: about 64 MB of flow per chunk (4 pairs at 1920 x 1080); debug mode
+// keeps the whole batch in one chunk (the stage dumps read the last call's
+// pairs).
+dis_status host_pipe_init(dis_ctx* c, int n)
+{
+    const size_t frame = (size_t)c->g.W * c->g.H;
+    int chunk = c->host_chunk > 0 ? c->host_chunk
+                                  : (int)std::max<size_t>(1, (size_t(64) << 20) / (frame * sizeof(float2)));
+    if (c->debug) chunk = std::max(chunk, n);
+    chunk = std::min(chunk, c->max_batch);
+    if (c->hp && c->hp->chunk == chunk) return DIS_OK;
+    c->hp.reset();
+    auto hp = std::make_unique<HostPipe>();
+    hp->chunk = chunk;
+    hp->frame = frame;
+    hp->device = c->device;
+    for (int s = 0; s < 2; ++s) {
+        if (hipMalloc(&hp->din[s], 2 * frame * chunk) != hipSuccess ||
+            hipMalloc(&hp->dout[s], sizeof(float2) * frame * chunk) != hipSuccess)
+            return fail(DIS_ERR_OUT_OF_MEMORY, "host-path device slot allocation failed");
+        DIS_HIP(hipEventCreateWithFlags(&hp->up_done[s], hipEventDisableTiming));
+        DIS_HIP(hipEventCreateWithFlags(&hp->comp_done[s], hipEventDisableTiming));
+        DIS_HIP(hipEventCreateWithFlags(&hp->down_done[s], hipEventDisableTiming));
+    }
+    DIS_HIP(hipStreamCreateWithFlags(&hp->up, hipStreamNonBlocking));
+    DIS_HIP(hipStreamCreateWithFlags(&hp->down, hipStreamNonBlocking));
+    HostPipe* raw = hp.get();
+    hp->th = std::thread([raw] { raw->run(); });
+    c->hp = std::move(hp);
+    return DIS_OK;
+}
+
+// dis_calc_batch_u8 on host frames and host flow. Chunk j: the calling thread
+// uploads it into device slot j % 2 (once the computation of chunk j-2 has
+// read that slot), enqueues its computation -- the device path on the
+// context's own stream, after the upload and after the download of chunk j-2
+// has read the output slot -- and posts its download to the download thread.
+// Pageable copies block the thread that issues them until they are done, so
+// the upload of chunk j+1 runs while chunk j computes and chunk j-1
+// downloads (PCIe is full duplex); page-locked caller buffers (dis_host_alloc,
+// hipHostMalloc / hipHostRegister) make every copy asynchronous. The flows are
+// the device path's, bit for bit.
+dis_status calc_host(dis_ctx* c, int n, const uint8_t* I0, const uint8_t* I1, size_t stride, size_t pair_stride,
+                     float* flow)
+{
+    dis_status st = host_pipe_init(c, n);
+    if (st != DIS_OK) return st;
+    HostPipe& P = *c->hp;
+    const int W = c->g.W, H = c->g.H, chunk = P.chunk;
+    const size_t fr = P.frame, fb = fr * sizeof(float2);
+    const size_t in_span = (size_t)(n - 1) * pair_stride + (size_t)(H - 1) * stride + W;
+    const bool pin_in = host_pinned(I0, in_span) && host_pinned(I1, in_span);
+    const bool pin_out = host_pinned(flow, fb * n);
+    const hipStream_t s = c->own;
+    const int nch = (n + chunk - 1) / chunk;
+    const long long base = P.posted;  // jobs of earlier calls (all issued and done)
+    auto drain = [&](hipError_t e0) -> dis_status {  // after an error: let the download thread finish
+        const hipError_t e1 = P.wait_issued(P.posted);
+        const hipError_t e = e0 != hipSuccess ? e0 : e1;
+        return fail(DIS_ERR_DEVICE, std::string("host-frame path: ") + hipGetErrorString(e));
+    };
+    for (int j = 0; j < nch; ++j) {
+        const int slot = j & 1, a = j * chunk, m = std::min(chunk, n - a);
+        uint8_t* din0 = P.din[slot];
+        uint8_t* din1 = P.din[slot] + (size_t)chunk * fr;
+        hipError_t e = hipSuccess;
+        // upload once the computation of chunk j-2 has read the slot
+        if (P.comp_pending[slot]) e = hipStreamWaitEvent(P.up, P.comp_done[slot], 0);
+        for (int k = 0; e == hipSuccess && k < m; ++k) {
+            e = hipMemcpy2DAsync(din0 + k * fr, W, I0 + (size_t)(a + k) * pair_stride, stride, W, H,
+                                 hipMemcpyHostToDevice, P.up);
+            if (e == hipSuccess)
+                e = hipMemcpy2DAsync(din1 + k * fr, W, I1 + (size_t)(a + k) * pair_stride, stride, W, H,
+                                     hipMemcpyHostToDevice, P.up);
+        }
+        if (e == hipSuccess) e = hipEventRecord(P.up_done[slot], P.up);
+        // compute after the upload and after the download of chunk j-2 (its
+        // job must have been issued for down_done[slot] to stand for it)
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, P.up_done[slot], 0);
+        if (e == hipSuccess && P.down_pending[slot]) {
+            e = P.wait_issued(base + j - 1);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, P.down_done[slot], 0);
+        }
+        if (e != hipSuccess) return drain(e);
+        // eager enqueue, not a replayed graph: this path is bound by PCIe (a
+        // chunk's download takes ~10x its computation), and launching a graph
+        // captured here crashed the HIP 7.2 runtime on the host in one call
+        // sequence (tools/repro_graph_steps.py EKSFH) that the
+        // eager form runs cleanly
+        {
+            std::lock_guard<std::mutex> lock(pool_mutex(c->device));
+            st = run_batches(c, m, din0, din1, (size_t)W, fr, P.dout[slot], s);
+        }
+        if (st != DIS_OK) {
+            drain(hipSuccess);
+            return st;
+        }
+        e = hipEventRecord(P.comp_done[slot], s);
+        if (e != hipSuccess) return drain(e);
+        P.comp_pending[slot] = true;
+        P.down_pending[slot] = true;
+        P.post({reinterpret_cast<char*>(flow) + (size_t)a * fb, reinterpret_cast<const char*>(P.dout[slot]), m * fb,
+                slot});
+    }
+    hipError_t e = P.wait_issued(base + nch);
+    if (e == hipSuccess) e = hipEventSynchronize(P.down_done[(nch - 1) & 1]);  // page-locked flow: the last copy
+    if (e != hipSuccess) return fail(DIS_ERR_DEVICE, std::string("host-frame path: ") + hipGetErrorString(e));
+    P.last_chunks = nch;
+    P.last_direct_in = pin_in ? 1 : 0;
+    P.last_direct_out = pin_out ? 1 : 0;
+    return DIS_OK;
+}
+
 // Sub-batch streams: one pool per device for the whole process, created
 // back to back on first use and never destroyed. HIP maps each new stream
 // onto one of its few hardware queues (GPU_MAX_HW_QUEUES = 4) by usage at
@@ -855,9 +1131,14 @@ struct CompatWs {
     int* fb = nullptr;
     size_t planes = 0, u = 0, d = 0, nfb = 0;
     hipStream_t stream = nullptr;
+    hipStream_t up = nullptr;                  // plane uploads, level by level
+    hipEvent_t level_up[dis::kMaxLevels] = {};  // level l's planes are on the device
     bool reserve(size_t p, size_t nu, size_t nd, size_t nf)
     {
         if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+        if (!up && hipStreamCreateWithFlags(&up, hipStreamNonBlocking) != hipSuccess) return false;
+        for (hipEvent_t& e : level_up)
+            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
         if (p > planes) {
             hipFree(dx);
             hipFree(dy);
@@ -1048,9 +1329,6 @@ dis_status dis_create(dis_ctx** out, const dis_params* params, int width, int he
               hipMalloc(&c->dx, plane) == hipSuccess && hipMalloc(&c->dy, plane) == hipSuccess &&
               hipMalloc(&c->pu, sizeof(float2) * (size_t)g.u_stride * B) == hipSuccess &&
               hipMalloc(&c->dense, sizeof(float2) * (size_t)g.dense_stride * B) == hipSuccess &&
-              hipMalloc(&c->in0, (size_t)width * height * B) == hipSuccess &&
-              hipMalloc(&c->in1, (size_t)width * height * B) == hipSuccess &&
-              hipMalloc(&c->out, sizeof(float2) * (size_t)width * height * B) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->done, hipEventDisableTiming) == hipSuccess;
@@ -1136,18 +1414,48 @@ dis_status dis_calc_batch_u8(dis_ctx* c, int n, const uint8_t* I0, const uint8_t
                                  reinterpret_cast<hipStream_t>(stream));
     }
     if (where != DIS_MEM_HOST) return fail(DIS_ERR_INVALID_ARGUMENT, "bad dis_mem");
-    hipStream_t s = c->own;
-    const size_t fsz = (size_t)W * H;
-    for (int k = 0; k < n; ++k) {
-        DIS_HIP(hipMemcpy2DAsync(c->in0 + k * fsz, W, I0 + k * pair_stride, stride, W, H,
-                                 hipMemcpyHostToDevice, s));
-        DIS_HIP(hipMemcpy2DAsync(c->in1 + k * fsz, W, I1 + k * pair_stride, stride, W, H,
-                                 hipMemcpyHostToDevice, s));
+    return calc_host(c, n, I0, I1, stride, pair_stride, flow);
+}
+
+dis_status dis_set_host_pipeline(dis_ctx* c, int chunk_pairs)
+{
+    if (!c) return fail(DIS_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (chunk_pairs < 0) return fail(DIS_ERR_INVALID_ARGUMENT, "chunk_pairs must be >= 0 (0 = auto)");
+    DIS_HIP(hipSetDevice(c->device));
+    c->hp.reset();  // rebuilt on the next host call (host calls are synchronous: nothing in flight)
+    c->host_chunk = chunk_pairs;
+    return DIS_OK;
+}
+
+dis_status dis_host_pipeline_info(dis_ctx* c, dis_host_info* out)
+{
+    if (!c || !out) return fail(DIS_ERR_INVALID_ARGUMENT, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    if (c->hp) {
+        out->chunk_pairs = c->hp->chunk;
+        out->last_chunks = c->hp->last_chunks;
+        out->last_direct_in = c->hp->last_direct_in;
+        out->last_direct_out = c->hp->last_direct_out;
     }
-    dis_status st = run_batches_graph(c, n, c->in0, c->in1, (size_t)W, fsz, c->out, s);
-    if (st != DIS_OK) return st;
-    DIS_HIP(hipMemcpyAsync(flow, c->out, sizeof(float2) * fsz * n, hipMemcpyDeviceToHost, s));
-    DIS_HIP(hipStreamSynchronize(s));
+    return DIS_OK;
+}
+
+dis_status dis_host_alloc(size_t bytes, void** out)
+{
+    if (!out) return fail(DIS_ERR_INVALID_ARGUMENT, "out is null");
+    *out = nullptr;
+    if (!bytes) return fail(DIS_ERR_INVALID_ARGUMENT, "bytes must be > 0");
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return fail(DIS_ERR_OUT_OF_MEMORY, "page-locked host allocation failed");
+    }
+    return DIS_OK;
+}
+
+dis_status dis_host_free(void* p)
+{
+    if (p && hipHostFree(p) != hipSuccess) return fail(DIS_ERR_INVALID_ARGUMENT, "not a dis_host_alloc pointer");
     return DIS_OK;
 }
 
@@ -1346,20 +1654,27 @@ dis_status dis_flow_from_pyramids(const float* const* img_first, const float* co
     if (!w.reserve(tot, g.u_stride, g.dense_stride, fb_n)) return fail(DIS_ERR_OUT_OF_MEMORY, "device allocation failed");
     hipStream_t s = w.stream;
     const bool fast = g.ps == 8;
-    auto H2D = [&](float* dst, const float* src, size_t cnt) {
-        return hipMemcpyAsync(dst, src, sizeof(float) * cnt, hipMemcpyHostToDevice, s);
-    };
-    for (int l = finest; l <= coarsest; ++l) {
-        const size_t cnt = (size_t)(g.lv[l].W + 2 * img_padding) * (g.lv[l].H + 2 * img_padding);
-        if (H2D(w.dx + poff[l], img_first_dx[l], cnt) != hipSuccess ||
-            H2D(w.dy + poff[l], img_first_dy[l], cnt) != hipSuccess ||
-            H2D(w.i1 + poff[l], img_second[l], cnt) != hipSuccess)
+    // The planes go up level by level, coarsest first, on a stream of their
+    // own; level l's search waits only for level l's planes. A pageable upload
+    // returns when it is done, so the finer (larger) levels' uploads run while
+    // the coarser levels search.
+    auto upload = [&](int l) {
+        const size_t bytes = sizeof(float) * (size_t)(g.lv[l].W + 2 * img_padding) * (g.lv[l].H + 2 * img_padding);
+        if (hipMemcpyAsync(w.dx + poff[l], img_first_dx[l], bytes, hipMemcpyHostToDevice, w.up) != hipSuccess ||
+            hipMemcpyAsync(w.dy + poff[l], img_first_dy[l], bytes, hipMemcpyHostToDevice, w.up) != hipSuccess ||
+            hipMemcpyAsync(w.i1 + poff[l], img_second[l], bytes, hipMemcpyHostToDevice, w.up) != hipSuccess ||
+            hipEventRecord(w.level_up[l], w.up) != hipSuccess || hipStreamWaitEvent(s, w.level_up[l], 0) != hipSuccess)
             return fail(DIS_ERR_DEVICE, "pyramid upload failed");
-    }
+        return DIS_OK;
+    };
+    // (the previous call's searches have read the workspace: `up` follows `s`)
+    DIS_HIP(hipEventRecord(w.level_up[g.C], s));
+    DIS_HIP(hipStreamWaitEvent(w.up, w.level_up[g.C], 0));
     if (fast) DIS_HIP(hipMemsetAsync(w.fb, 0, sizeof(int) * dis::kMaxLevels, s));
     size_t fb_off = dis::kMaxLevels;
     for (int l = g.C; l >= g.F; --l) {
         const dis::LevelGeom& L = g.lv[l];
+        if (dis_status us = upload(l); us != DIS_OK) return us;
         if (fast) {  // the patch_size-8 search on the caller's planes (Search8Args.gdx_plane)
             dis::Search8Args b{};
             b.img1 = w.i1;

@@ -57,7 +57,8 @@ EXPORTED_SYMBOLS = (
     "dis_flow_from_pyramids", "dis_set_debug", "dis_stage_size", "dis_debug_dump",
     "dis_set_kernel_timing", "dis_kernel_time", "dis_synth_pair", "dis_set_kernel_variant",
     "dis_set_concurrency", "dis_set_precision", "dis_set_graphs", "dis_flow_color", "dis_flo_info",
-    "dis_read_flo", "dis_write_flo", "dis_build_kind",
+    "dis_read_flo", "dis_write_flo", "dis_build_kind", "dis_set_host_pipeline", "dis_host_pipeline_info",
+    "dis_host_alloc", "dis_host_free", "dis_batch_stream_plan", "dis_check_stream_plan",
 )
 
 
@@ -86,6 +87,10 @@ class _Params(ctypes.Structure):
         ("var_refine_iters", ctypes.c_int),
         ("paper_mode", ctypes.c_int),
     ]
+
+
+class _HostInfo(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in ("chunk_pairs", "last_chunks", "last_direct_in", "last_direct_out")]
 
 
 class _Workload(ctypes.Structure):
@@ -155,6 +160,13 @@ def lib() -> ctypes.CDLL:
             L.dis_set_graphs.argtypes = [V, I]
         if L.dis_abi_version() >= 6:
             L.dis_build_kind.restype = ctypes.c_char_p
+        if L.dis_abi_version() >= 8:
+            L.dis_set_host_pipeline.argtypes = [V, I]
+            L.dis_host_pipeline_info.argtypes = [V, P(_HostInfo)]
+            L.dis_host_alloc.argtypes = [Z, P(V)]
+            L.dis_host_free.argtypes = [V]
+            L.dis_batch_stream_plan.argtypes = [I, I, P(I), I, P(I)]
+            L.dis_check_stream_plan.argtypes = [P(I), I, I, I]
         L.dis_stage_size.argtypes = [V, I, I, P(Z)]
         L.dis_debug_dump.argtypes = [V, I, I, I, V, Z]
         L.dis_set_kernel_timing.argtypes = [V, I]
@@ -233,6 +245,25 @@ def write_flo(path: str, data: np.ndarray) -> None:
     _check(lib().dis_write_flo(os.fsencode(path), _ptr(d), d.shape[1], d.shape[0], d.shape[2]))
 
 
+def batch_stream_plan(nsub: int, nstages: int) -> list:
+    """The fork / stage / join ops a batch call with nsub sub-batches issues
+    (dis_batch_stream_plan): list of (kind, stream, event, stage)."""
+    n = ctypes.c_int()
+    _check(lib().dis_batch_stream_plan(nsub, nstages, None, 0, ctypes.byref(n)))
+    buf = (ctypes.c_int * (4 * n.value))()
+    _check(lib().dis_batch_stream_plan(nsub, nstages, buf, n.value, ctypes.byref(n)))
+    return [tuple(buf[4 * i:4 * i + 4]) for i in range(n.value)]
+
+
+def check_stream_plan(ops, nstreams: int, nevents: int) -> str | None:
+    """None if the plan keeps the capture rules (dis_check_stream_plan), else
+    the broken rule."""
+    flat = [int(v) for op in ops for v in op]
+    buf = (ctypes.c_int * max(1, len(flat)))(*flat)
+    st = lib().dis_check_stream_plan(buf, len(ops), nstreams, nevents)
+    return None if st == DIS_OK else lib().dis_last_error().decode()
+
+
 def synth_pair(seed: int, width: int, height: int, with_gt: bool = False):
     """Deterministic synthetic u8 pair (and ground-truth flow) for seed."""
     I0 = np.empty((height, width), np.uint8)
@@ -285,6 +316,23 @@ class DenseInverseSearch:
         """Asynchronous calc on device-resident buffers (raw device pointers)."""
         _check(lib().dis_calc_batch_u8(self._ctx, n, I0_ptr, I1_ptr, stride, pair_stride, flow_ptr,
                                        MEM_DEVICE, stream or None))
+
+    def set_host_pipeline(self, chunk_pairs: int = 0) -> None:
+        """dis_set_host_pipeline: pairs per chunk of a host-memory batch call
+        (0 = auto, about 64 MB of flow); results are identical."""
+        _check(lib().dis_set_host_pipeline(self._ctx, chunk_pairs))
+
+    def host_pipeline_info(self) -> dict:
+        """What the last host-memory call did (chunks, direct DMA of page-locked buffers)."""
+        h = _HostInfo()
+        _check(lib().dis_host_pipeline_info(self._ctx, ctypes.byref(h)))
+        return {k: getattr(h, k) for k, _ in _HostInfo._fields_}
+
+    def calc_batch_host(self, n: int, I0_ptr: int, I1_ptr: int, flow_ptr: int, stride: int = 0,
+                        pair_stride: int = 0) -> None:
+        """dis_calc_batch_u8 on raw host pointers (pageable or page-locked), synchronous."""
+        _check(lib().dis_calc_batch_u8(self._ctx, n, I0_ptr, I1_ptr, stride, pair_stride, flow_ptr,
+                                       MEM_HOST, None))
 
     def set_variant(self, variant: int) -> None:
         """dis_set_kernel_variant (include/dis_abi.h): 0 = auto (specialised kernels),

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(disflow_mod):
     L = disflow_mod.lib()
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert L.dis_abi_version() == 7
+    assert L.dis_abi_version() == 8
     assert not hasattr(L, "dis_pipeline_link")  # removed in v6
 
 

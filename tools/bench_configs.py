@@ -18,6 +18,10 @@ resident in HBM, batch per call as given, `steps` timed calls after warmup.
   compat    1920x1080  MEDIUM through the reference-interface entry (dis_flow_from_pyramids,
             OpticalFlowClass semantics: host padded pyramids in, finest-level flow out,
             synchronous) beside dis_calc_u8 on host frames, one pair per call
+  host      1920x1080  MEDIUM host-frame path (dis_calc_batch_u8 with DIS_MEM_HOST: host
+            frames in, host flow out, synchronous) at batches 1, 4 and 32, pageable and
+            page-locked buffers, beside the box's measured D2H rate and the pairs/s that
+            rate allows for 16.6 MB of flow per pair
 """
 import argparse
 import json
@@ -186,6 +190,51 @@ def run_compat(steps, warmup):
                     "full-resolution flow D2H)"}
 
 
+def run_host(steps, warmup):
+    W, H, Bmax = 1920, 1080, 32
+    dev = torch.device("cuda", 0)
+    p = disflow.preset_params(disflow.Preset.MEDIUM, W, H)
+    pairs = [disflow.synth_pair(k, W, H) for k in range(Bmax)]
+    I0 = np.stack([a for a, _ in pairs])
+    I1 = np.stack([b for _, b in pairs])
+    fb = W * H * 8
+    # the box's D2H rate: page-locked destination, 4 pairs' flow per copy
+    d = torch.empty(4 * fb, dtype=torch.uint8, device=dev)
+    h = torch.empty(4 * fb, dtype=torch.uint8, pin_memory=True)
+    h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = 10 * 4 * fb / (time.perf_counter() - t0) / 1e9
+    del d, h
+    eng = disflow.DenseInverseSearch(p, W, H, max_batch=Bmax)
+    flow = np.empty((Bmax, H, W, 2), np.float32)
+    pf = torch.empty((Bmax, H, W, 2), dtype=torch.float32, pin_memory=True)
+    pi0 = torch.from_numpy(I0).pin_memory()
+    pi1 = torch.from_numpy(I1).pin_memory()
+    res = {}
+    for kind, a0, a1, fo in (("pageable", I0.ctypes.data, I1.ctypes.data, flow.ctypes.data),
+                             ("page_locked", pi0.data_ptr(), pi1.data_ptr(), pf.data_ptr())):
+        for B in (1, 4, 32):
+            for _ in range(max(1, warmup)):
+                eng.calc_batch_host(B, a0, a1, fo)
+            reps = max(2, steps * 4 // B)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                eng.calc_batch_host(B, a0, a1, fo)
+            res[f"{kind}_B{B}"] = B * reps / (time.perf_counter() - t0)
+    info = eng.host_pipeline_info()
+    eng.close()
+    bound = d2h * 1e9 / fb
+    return {"config": "host-frame path 1920x1080 MEDIUM (dis_calc_batch_u8, DIS_MEM_HOST)",
+            "pairs_per_s": res, "d2h_GBps": d2h, "d2h_bound_pairs_per_s": bound,
+            "frac_of_d2h_bound": {k: v / bound for k, v in res.items()}, "pipeline": info,
+            "note": "d2h = page-locked 66 MB copies on this box; the bound = that rate / 16.6 MB of flow per pair "
+                    "(the uploads, 4.1 MB per pair, run the other PCIe direction)"}
+
+
 def run_cpu1(budget_s):
     """BASELINE config 1 on the host: 640x480 ULTRAFAST through the C
     restatement, single-core latency and 16-process throughput (bench.py's
@@ -206,7 +255,7 @@ def run_cpu1(budget_s):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1cpu,1,2,3,5,2p,2f,3f,colour,compat")
+    ap.add_argument("--configs", default="1cpu,1,2,3,5,2p,2f,3f,colour,compat,host")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=9.0)
@@ -220,6 +269,8 @@ def main():
             r = run_colour(a.steps, a.warmup)
         elif c == "compat":
             r = run_compat(a.steps, a.warmup)
+        elif c == "host":
+            r = run_host(a.steps, a.warmup)
         else:
             name, W, H, preset, B = CONFIGS[c][:5]
             steps = max(2, a.steps // (4 if c == "5" else 1))

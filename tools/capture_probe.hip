@@ -15,6 +15,11 @@
 //      same event object is re-recorded on s1 afterwards (event reuse)
 //   5  capture ends with s1 forked but never joined back (unjoined)
 //   6  an uncaptured stream waits on an event recorded inside the capture
+//   7  s1 joined back only through s0 (s0 waits on s1's last record, the
+//      origin waits on s0's): a transitive join
+//   8  as 5, then hipGraphDestroy of the handle the failed EndCapture wrote
+//      (what run_batches_graph did with it until r06)
+//   9  as 5, then a kernel launch and a synchronise on the unjoined stream
 //
 // Prints each call's status; exit 0 when the sequence ran to the end (whatever
 // the statuses), so a host crash shows as the process's signal.
@@ -41,6 +46,7 @@ static void status(const char* what, hipStream_t s)
     unsigned long long id = 0;
     hipError_t e = hipStreamGetCaptureInfo(s, &st, &id);
     std::printf("  capture status of %-6s: %d (id %llu, %s)\n", what, (int)st, id, hipGetErrorName(e));
+    std::fflush(stdout);
 }
 
 int main(int argc, char** argv)
@@ -93,7 +99,13 @@ int main(int argc, char** argv)
     }
     CALL(hipEventRecord(j0, s0));
     CALL(hipStreamWaitEvent(cap, j0, 0));
-    if (mode != 3 && mode != 5) {
+    if (mode == 7) {  // s1 -> s0 (before s0's join record above is replaced by a later one)
+        CALL(hipEventRecord(j1, s1));
+        CALL(hipStreamWaitEvent(s0, j1, 0));
+        CALL(hipEventRecord(j0, s0));
+        CALL(hipStreamWaitEvent(cap, j0, 0));
+    }
+    if (mode != 3 && mode != 5 && mode != 7 && mode != 8 && mode != 9) {
         CALL(hipEventRecord(j1, s1));
         CALL(hipStreamWaitEvent(cap, j1, 0));
     }
@@ -101,7 +113,24 @@ int main(int argc, char** argv)
     hipGraph_t g = nullptr;
     CALL(hipStreamEndCapture(cap, &g));
     std::printf("  graph %p\n", (void*)g);
+    std::fflush(stdout);
     status("s1 after", s1);
+    if (mode == 8) {
+        CALL(hipGraphDestroy(g));
+        std::printf("mode 8 done\n");
+        return 0;
+    }
+    if (mode == 9) {
+        hipLaunchKernelGGL(k_add, dim3(1), dim3(64), 0, s1, d, 1.f);
+        CALL(hipGetLastError());
+        CALL(hipStreamSynchronize(s1));
+        std::printf("mode 9 done\n");
+        return 0;
+    }
+    if (mode == 5) {  // the failed EndCapture's handle is not used
+        std::printf("mode 5 done\n");
+        return 0;
+    }
     if (g) {
         hipGraphExec_t x = nullptr;
         CALL(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));

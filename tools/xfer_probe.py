@@ -40,6 +40,8 @@ def main():
     hp = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
     hq = torch.empty(nb, dtype=torch.uint8)
     hq.fill_(1)
+    lib = os.environ.get("DISFLOW_LIB")
+    out["lib"] = os.path.basename(lib) if lib else "libdis_hip.so"
     for k, fn in (("pinned_d2h_GBps", lambda: hp.copy_(d, non_blocking=True)),
                   ("pinned_h2d_GBps", lambda: d.copy_(hp, non_blocking=True)),
                   ("pageable_d2h_GBps", lambda: hq.copy_(d)),
@@ -109,6 +111,21 @@ def main():
             callp()
         hostp[B] = B * reps / (time.perf_counter() - t0)
     out["host_mode_pinned_pairs_per_s"] = hostp
+    # chunk sizes at B = 32, pageable buffers (the library default: 0 = auto)
+    sweep = {}
+    flow = np.empty((Bmax, H, W, 2), np.float32)
+    for chunk in (1, 2, 4, 8, 0):
+        try:
+            eng.set_host_pipeline(chunk)
+        except Exception as e:  # (an A/B library with another setter)
+            sweep[f"chunk{chunk}"] = repr(e)[:60]
+            continue
+        eng.calc_batch_host(Bmax, I0.ctypes.data, I1.ctypes.data, flow.ctypes.data)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            eng.calc_batch_host(Bmax, I0.ctypes.data, I1.ctypes.data, flow.ctypes.data)
+        sweep[f"chunk{chunk}"] = 3 * Bmax / (time.perf_counter() - t0)
+    out["host_mode_sweep_B32"] = sweep
     out["d2h_bound_pairs_per_s"] = out["pinned_d2h_GBps"] * 1e9 / nb
     eng.close()
     print(json.dumps(out))
