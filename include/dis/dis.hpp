@@ -106,6 +106,8 @@ public:
     // DIS_PRECISION_EXACT (default) or DIS_PRECISION_FMA (dis_abi.h)
     void set_precision(int mode) { check(dis_set_precision(ctx_, mode)); }
     void set_graphs(bool on) { check(dis_set_graphs(ctx_, on ? 1 : 0)); }
+    // host-memory batches: pairs per overlapped chunk (0 = auto), ABI v8
+    void set_host_pipeline(int chunk_pairs) { check(dis_set_host_pipeline(ctx_, chunk_pairs)); }
 
     const dis_params& params() const { return params_; }
     int width() const { return width_; }
