@@ -55,6 +55,12 @@ std::string check_capture_plan(const PlanOp* ops, int n, int nstreams, int neven
                               o.stream, o.event);
                 return b;
             }
+            if (o.stream != 0 && ops[r].stream != 0) {
+                std::snprintf(b, sizeof b,
+                              "op %d: sub-batch stream %d waits on event %d of sub-batch stream %d: a sibling edge (R5)",
+                              i, o.stream, o.event, ops[r].stream);
+                return b;
+            }
             for (size_t x = 0; x < S; ++x) vc[i][x] = std::max(vc[i][x], vc[r][x]);
             member[o.stream] = 1;  // R1
         } else if (!member[o.stream]) {

@@ -29,22 +29,24 @@ std::vector<PlanOp> batch_plan(int S, int nstages);
 
 // Whether `ops` can be captured from the origin stream (empty string) or what
 // breaks the rules, each measured on HIP 7.2 / gfx950 (tools/capture_probe.hip,
-// DESIGN.md 5b):
+// tools/repro_sibling_capture.sh):
 //  R1 a stream joins the capture by waiting on an event recorded in it (fork);
 //  R2 every wait is on an event recorded earlier in the same capture: a wait
 //     on an event recorded before the capture began is accepted and silently
 //     dropped from the graph (the dependency is lost, probe mode 3);
 //  R3 work and records only on streams in the capture;
 //  R4 at the end every stream that joined has been joined back: all of its
-//     operations happen before the origin's last one, directly or through
-//     other streams (probe mode 7). An unjoined stream makes
-//     hipStreamEndCapture fail with hipErrorStreamCaptureUnjoined, leaves
-//     that stream in capture mode (a later synchronise on it fails,
-//     mode 9) and writes a non-null handle that is not a graph (instantiating
-//     it crashed the probe's host process, mode 5 of the first probe run;
-//     destroying it returns hipErrorIllegalState, mode 8).
-// Sibling edges (one sub-batch stream waiting on another's event) are legal
-// and captured correctly (probe modes 2 and 7).
+//     operations happen before the origin's last one. An unjoined stream makes
+//     hipStreamEndCapture fail with hipErrorStreamCaptureUnjoined, leaves that
+//     stream in capture mode (a later synchronise on it fails, mode 9) and
+//     writes a non-null handle that is not a graph (instantiating it crashed
+//     the probe's process; destroying it returns hipErrorIllegalState);
+//  R5 no sibling edge: a sub-batch stream waits only on events the origin
+//     recorded. The product's capture with one mid-call barrier between the
+//     sub-batch streams SIGSEGVs inside hipStreamEndCapture, with the join
+//     events reused or with events of its own, while the eager call runs and
+//     small probe graphs of the same shape capture fine (modes 2, 7, 10-13) --
+//     the r05 crash (its merged finest launch waited on sibling events).
 std::string check_capture_plan(const PlanOp* ops, int n, int nstreams, int nevents);
 
 }  // namespace dis

@@ -1,10 +1,11 @@
 """The batch call's stream plan and the HIP-graph capture rules (CPU only:
 dis_batch_stream_plan / dis_check_stream_plan need no device). The rules were
-measured on HIP 7.2 with tools/capture_probe.hip: a sub-batch
-stream left unjoined makes hipStreamEndCapture fail, leaves the stream in
-capture mode and writes a handle that is not a graph (instantiating it crashed
-the host process); a wait on an event recorded before the capture is silently
-dropped from the graph."""
+measured on HIP 7.2 with tools/capture_probe.hip and
+tools/repro_sibling_capture.sh: a sub-batch stream left
+unjoined makes hipStreamEndCapture fail, leaves the stream in capture mode and
+writes a handle that is not a graph; a wait on an event recorded before the
+capture is silently dropped from the graph; a sibling edge between sub-batch
+streams crashes hipStreamEndCapture on the product's graph (the r05 crash)."""
 import pytest
 
 REC, WAIT, WORK = 0, 1, 2
@@ -44,15 +45,21 @@ def test_work_after_the_join_is_refused(d):
     assert "R4" in d.check_stream_plan(ops, 2, 2)
 
 
-def test_transitive_join_and_sibling_edges_are_legal(d):
-    # probe modes 2 and 7: sub 1 waits on sub 0 and the other way round; sub 1
-    # joins back only through sub 0
+def test_sibling_edges_are_refused(d):
+    # a barrier between the sub-batch streams in the middle of the call: HIP 7.2
+    # crashes inside hipStreamEndCapture on the product's graph with it
+    # (tools/repro_sibling_capture.sh; the r05 crash), so the checker refuses
+    # any wait of a sub-batch stream on another sub-batch stream's event
     ops = _fork(2) + [(WORK, 1, -1, 0), (WORK, 2, -1, 0),
-                      (REC, 2, 2, -1), (WAIT, 1, 2, -1), (WORK, 1, -1, 1),
-                      (REC, 1, 1, -1), (WAIT, 2, 1, -1), (WORK, 2, -1, 1),
-                      (REC, 2, 2, -1), (WAIT, 1, 2, -1),
+                      (REC, 1, 1, -1), (REC, 2, 2, -1), (WAIT, 1, 2, -1), (WAIT, 2, 1, -1),
+                      (WORK, 1, -1, 1), (WORK, 2, -1, 1),
+                      (REC, 1, 1, -1), (WAIT, 0, 1, -1), (REC, 2, 2, -1), (WAIT, 0, 2, -1)]
+    why = d.check_stream_plan(ops, 3, 3)
+    assert why and "R5" in why and "sibling" in why
+    # a transitive join is one too
+    ops = _fork(2) + [(WORK, 1, -1, 0), (WORK, 2, -1, 0), (REC, 2, 2, -1), (WAIT, 1, 2, -1),
                       (REC, 1, 1, -1), (WAIT, 0, 1, -1)]
-    assert d.check_stream_plan(ops, 3, 3) is None
+    assert "R5" in d.check_stream_plan(ops, 3, 3)
 
 
 def test_stale_event_is_refused(d):

@@ -20,6 +20,14 @@
 //   8  as 5, then hipGraphDestroy of the handle the failed EndCapture wrote
 //      (what run_batches_graph did with it until r06)
 //   9  as 5, then a kernel launch and a synchronise on the unjoined stream
+//  10  a barrier between the siblings, then the join with the SAME events:
+//      s0 records j0, s1 records j1, each waits on the other's, more kernels,
+//      then j0 / j1 are recorded again and the origin waits on them (the
+//      product's plan with a mid-call sub-batch barrier)
+//  11  as 10 with distinct events for the barrier and the join
+//  12  as 10 with the product's shape: 5 kernels per stream before the
+//      barrier and 7 after, each with a 256-byte argument block
+//  13  as 12 with distinct barrier events
 //
 // Prints each call's status; exit 0 when the sequence ran to the end (whatever
 // the statuses), so a host crash shows as the process's signal.
@@ -31,6 +39,16 @@
 __global__ void k_add(float* p, float v)
 {
     p[threadIdx.x] += v;
+}
+
+struct BigArgs {
+    float* p;
+    float v;
+    int pad[60];
+};
+__global__ void k_big(BigArgs a)
+{
+    a.p[threadIdx.x] += a.v + (float)a.pad[threadIdx.x & 31];
 }
 
 #define CALL(x)                                                                       \
@@ -91,6 +109,31 @@ int main(int argc, char** argv)
         CALL(hipStreamWaitEvent(s0, mid1, 0));  // stale event, s1 outside the capture
         status("s1", s1);
         hipLaunchKernelGGL(k_add, dim3(1), dim3(64), 0, s0, d + 128, 2.f);
+    }
+    BigArgs ba{};
+    ba.v = 0.f;
+    if (mode == 12 || mode == 13) {
+        for (int k = 0; k < 5; ++k) {
+            ba.p = d;
+            hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s0, ba);
+            ba.p = d + 64;
+            hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s1, ba);
+        }
+    }
+    if (mode >= 10 && mode <= 13) {
+        hipEvent_t b0 = (mode == 10 || mode == 12) ? j0 : mid0, b1 = (mode == 10 || mode == 12) ? j1 : mid1;
+        CALL(hipEventRecord(b0, s0));
+        CALL(hipEventRecord(b1, s1));
+        CALL(hipStreamWaitEvent(s0, b1, 0));
+        CALL(hipStreamWaitEvent(s1, b0, 0));
+        hipLaunchKernelGGL(k_add, dim3(1), dim3(64), 0, s0, d + 128, 2.f);
+        hipLaunchKernelGGL(k_add, dim3(1), dim3(64), 0, s1, d + 192, 2.f);
+        for (int k = 0; mode >= 12 && k < 6; ++k) {
+            ba.p = d + 128;
+            hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s0, ba);
+            ba.p = d + 192;
+            hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s1, ba);
+        }
     }
     if (mode == 6) {
         CALL(hipEventRecord(mid0, s0));
