@@ -5,7 +5,7 @@
 // order, -ffp-contract=off, so the results are bit-identical).
 //
 // Two launches per fixed-point iteration (re-warp, linearise, red-black SOR):
-//   k_vr_lin  one 64x16 tile of pixels: I1 warped by the current flow over the
+//   k_vr_lin  one 32x32 tile of pixels: I1 warped by the current flow over the
 //             tile +-4 (bilinear, replicate border), its 5-tap derivatives over
 //             the tile +-2, the smoothness weights alpha/sqrt(|grad u|^2 +
 //             |grad v|^2 + eps^2) over the tile + its left column / top row --
