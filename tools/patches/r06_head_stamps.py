@@ -1,3 +1,5 @@
+# r06 experiment: per-workgroup s_memrealtime stamps for the coarse-head patch
+# (tools/build_head_variant.sh with STAMPS=1 applies it; tools/head_probe.py reads them).
 p = "csrc/dis_search8.hip"; s = open(p).read()
 old = "typedef __attribute__((address_space(1))) int g_i32;"
 assert old in s

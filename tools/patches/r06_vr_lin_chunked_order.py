@@ -1,3 +1,5 @@
+# r06 experiment (not kept): k_vr_lin tiles in a chunked XCD order (each XCD
+# a run of R = 8 tiles along x). Run in the package directory of a /tmp copy of the tree.
 p = "csrc/dis_varref.hip"; s = open(p).read()
 old = """    const int W = L.W, H = L.H, pr = blockIdx.z, tid = threadIdx.x;
     const int x0 = blockIdx.x * kLW, y0 = blockIdx.y * kLH;"""

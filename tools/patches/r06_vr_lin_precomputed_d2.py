@@ -1,3 +1,6 @@
+# r06 experiment (not kept): I0's second derivatives precomputed once per level
+# (k_vr_d1) so k_vr_lin stages no I0x / I0y halo in LDS. Run in the package directory of a /tmp
+# copy of the tree, then build there (make ROOT=... BUILD=... LIB=...); argument w5: 5 waves per SIMD.
 import sys
 p = "csrc/dis_kernels.h"; s = open(p).read()
 old = "constexpr int kVarRefPlanes = 8;"; assert old in s
