@@ -563,10 +563,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             for (int r0 = wave; r0 < RH; r0 += 8 * NW) {
                 float v[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int r = r0 + NW * j;
-                    v[j] = (r < RH && col < RW) ? I0[(size_t)clampi(reflect101(y0 + r, H), 0, H - 1) * W + c0]
-                                                : 0.0f;
+                for (int j = 0; j < 8; ++j) {  // unconditional (clamped) loads; the stores are masked
+                    const int r = min(r0 + NW * j, RH - 1);
+                    v[j] = I0[(size_t)clampi(reflect101(y0 + r, H), 0, H - 1) * W + c0];
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -879,9 +878,9 @@ __device__ __forceinline__ void search_block(const Search8Args& a, int bxi, int 
             for (int r0 = wave; r0 < th; r0 += kTileGroup * NW) {
                 float v[kTileGroup];
 #pragma unroll
-                for (int j = 0; j < kTileGroup; ++j) {
-                    const int r = r0 + NW * j;
-                    v[j] = (r < th && col < tw) ? I1[(ptrdiff_t)clampi(ty0 + r, lo, H - 1 + pad) * ld + cx] : 0.0f;
+                for (int j = 0; j < kTileGroup; ++j) {  // unconditional (clamped) loads; the stores are masked
+                    const int r = min(r0 + NW * j, th - 1);
+                    v[j] = I1[(ptrdiff_t)clampi(ty0 + r, lo, H - 1 + pad) * ld + cx];
                 }
 #pragma unroll
                 for (int j = 0; j < kTileGroup; ++j) {
