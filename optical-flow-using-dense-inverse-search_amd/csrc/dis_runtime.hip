@@ -214,6 +214,9 @@ struct HostPipe {
             cv.notify_all();
             th.join();
         }
+        // copies of a call that failed part-way may still be in flight
+        if (up) (void)hipStreamSynchronize(up);
+        if (down) (void)hipStreamSynchronize(down);
         for (int s = 0; s < 2; ++s) {
             hipFree(din[s]);
             hipFree(dout[s]);
